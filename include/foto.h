@@ -1,0 +1,157 @@
+/*
+ * libfoto -- MI355X-native FOTO hot path (Benamou-Brenier dynamic-OT optical flow
+ * solver + the Gennert-Negahdaripour variational baseline) behind a plain C ABI.
+ *
+ * Every entry point takes caller-owned HOST buffers (float64, row-major, the layout
+ * of the reference: voxel k = n*Nx*Ny + j*Nx + i, 3-field vectors SoA
+ * [t-part; x-part; y-part]) and returns 0 on success, < 0 on error
+ * (foto_last_error() has the message).  Each declaration cites the reference
+ * interface it replaces (paths relative to the reference repository root).
+ *
+ * The reference is pure Python (numpy/scipy); its "FFI" for this path is the
+ * Python call surface.  The binding a maintainer adds is the ctypes layer in
+ * optical-flow-optimal-transport_amd/foto/_lib.py.
+ */
+#ifndef FOTO_H
+#define FOTO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FOTO_OK 0
+#define FOTO_ERR_ARG (-1)     /* bad sizes / arguments (reference: IndexError, ZeroDivisionError) */
+#define FOTO_ERR_HIP (-2)     /* HIP runtime error (no device, OOM, launch failure)              */
+#define FOTO_ERR_COMM (-3)    /* RCCL error                                                      */
+#define FOTO_ERR_STATE (-4)   /* call out of order (e.g. flow before any iteration)              */
+#define FOTO_ERR_BC (-5)      /* boundary condition not in {'N','D'}: NotImplementedError        */
+
+const char* foto_last_error(void);
+int foto_version(void);
+int foto_device_count(int* n);
+
+/* ------------------------------------------------------------------ operators
+ * Matrix-free applications of the sparse operators of operators.py (h = 1).   */
+
+/* operators.grad_st(Nt,Nx,Ny,1,1,1,'N') @ phi  (operators.py:114-127)       -> out3[3N] */
+int foto_grad_st(const double* phi, int Nt, int Nx, int Ny, double* out3);
+/* operators.div_st(Nt,Nx,Ny,1,1,1,'N') @ w3    (operators.py:129-142)       -> out[N]   */
+int foto_div_st(const double* w3, int Nt, int Nx, int Ny, double* out);
+/* operators.laplacian_st(Nt,Nx,Ny,1,1,1,'N') @ p (operators.py:144-157)     -> out[N]   */
+int foto_laplacian_st(const double* p, int Nt, int Nx, int Ny, double* out);
+/* (-r*L_st + r*eps*I) @ p                      (benamou_brenier.py:202-203) -> out[N]   */
+int foto_apply_A(const double* p, int Nt, int Nx, int Ny, double r, double eps, double* out);
+/* operators.grad(Nx,Ny,1,1,bc) @ f             (operators.py:160-169)       -> out2[2*Nx*Ny] */
+int foto_grad2(const double* f, int Nx, int Ny, char bc, double* out2);
+/* operators.div(Nx,Ny,1,1,bc) @ [u;v]          (operators.py:182-191)       -> out[Nx*Ny] */
+int foto_div2(const double* uv, int Nx, int Ny, char bc, double* out);
+/* operators.grad_forward(Nx,Ny,1,1,'N') @ f    (operators.py:171-180)       -> out2[2*Nx*Ny] */
+int foto_grad2_forward(const double* f, int Nx, int Ny, double* out2);
+
+/* ------------------------------------------------------------------ BB building blocks */
+
+/* benamou_brenier.stepB(p, ...)  (benamou_brenier.py:93-149); M = Nt*Nx*Ny        */
+int foto_stepB(const double* p3, int64_t M, double* q3);
+/* RHS of solve_benamou_brenier_step: div_st(mu - r q) + temporal BC correction
+ * (benamou_brenier.py:64-82)                                                       */
+int foto_bb_rhs(const double* mu3, const double* q3, const double* rho0, const double* rhoT,
+                int Nt, int Nx, int Ny, double r, double* F);
+/* scipy.sparse.linalg.cg(A, b, rtol, maxiter) with A = -r L_st + r eps I, x0 = 0
+ * (benamou_brenier.py:85).  Returns info (0 converged, maxiter otherwise) or < 0;
+ * *iterations = CG iterations run.  mode: 0 = stencil CG, 1 = spectral CG.        */
+int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double eps, double rtol, int maxiter,
+            int mode, double* x, int* iterations);
+/* utils.opticalflow_from_benamoubrenier(phi, Nt, Nx, Ny, grad('N'), div('D'))
+ * (utils.py:44-99, 148-183)                                                        */
+int foto_flow_from_phi(const double* phi, int Nt, int Nx, int Ny, double* u, double* v, double* m);
+
+/* ------------------------------------------------------------------ BB solver context
+ * benamou_brenier.solve (benamou_brenier.py:151-271) split into create / iterate /
+ * flow so a caller can keep the state resident in HBM between calls.             */
+typedef struct foto_bb_ctx foto_bb_ctx;
+
+typedef struct {
+    int device;           /* HIP device ordinal; -1 = current device                       */
+    int cg_maxiter;       /* 1000 (benamou_brenier.py:85)                                  */
+    double cg_rtol;       /* 1e-6 (benamou_brenier.py:85)                                  */
+    int cg_mode;          /* 0 = stencil CG (7-point matvec), 1 = spectral CG (DCT basis)  */
+    int rank, world;      /* time-slab sharding over `world` processes (RCCL); 1 = single  */
+    const void* nccl_id;  /* 128-byte ncclUniqueId (foto_nccl_unique_id on rank 0)         */
+    int virtual_ranks;    /* >1: shard over this many in-process slabs on ONE device       */
+                          /* (tests the sharded path without RCCL; world must be 1)       */
+    int timing;           /* 1: time every kernel launch with HIP events (foto_bb_stats)   */
+} foto_bb_opts;
+
+/* per outer iteration: crit and the CG iteration count / info of that stepA */
+typedef void (*foto_bb_iter_cb)(void* user, int iter, double crit, int cg_iters, int cg_info);
+
+typedef struct {
+    int outer_iters;          /* outer iterations completed so far                      */
+    int64_t cg_iters_total;   /* CG iterations over all outer iterations                */
+    double last_crit;
+    double ms_rhs, ms_cg, ms_prox, ms_flow;   /* phase wall time (HIP events)           */
+    /* per kernel class (timing = 1): launches and summed device time in ms            */
+    int64_t n_k[8];
+    double ms_k[8];
+    double bytes_k[8];        /* algorithmic HBM bytes per launch of that class         */
+} foto_bb_stats;
+
+/* kernel classes reported in foto_bb_stats.n_k / ms_k / bytes_k */
+#define FOTO_K_CG_DIR    0   /* stencil CG: p = r + beta p, A p, p.Ap                    */
+#define FOTO_K_CG_UPD    1   /* stencil CG: x += alpha p, r -= alpha A p, r.r            */
+#define FOTO_K_RHS       2   /* div_st(mu - r q) + BC                                    */
+#define FOTO_K_PROX      3   /* grad_st phi, stepB, mu update, crit sums                 */
+#define FOTO_K_SPEC      4   /* spectral CG iteration kernel(s)                          */
+#define FOTO_K_DCT       5   /* DCT-II transforms                                        */
+#define FOTO_K_FLOW      6   /* trajectory integration + divergence                      */
+#define FOTO_K_OTHER     7
+
+int foto_bb_opts_default(foto_bb_opts* o);
+int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r,
+                   double reg_epsilon, const foto_bb_opts* opts, foto_bb_ctx** out);
+/* Run up to `max_iters` outer iterations (stepA + stepB + stepC + criterion).  With
+ * use_stop_rules = 1 it stops like the reference (crit <= tol, or |dcrit| < 1e-5).
+ * `total_max_it` is the max_it printed by the reference's "(i/max_it)" line and
+ * passed to cb only for numbering.  Returns 1 if a stop rule fired, 0 otherwise.  */
+int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double convergence_tol, int use_stop_rules,
+                    foto_bb_iter_cb cb, void* user, int* iters_done);
+/* Flow (u, v, m) from the last phi: utils.opticalflow_from_benamoubrenier.
+ * With world > 1 the result lands on rank 0; other ranks may pass NULL.           */
+int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m);
+/* Copy this shard's slab range of phi / mu / q to host (t0, nloc via foto_bb_shard). */
+int foto_bb_get_phi(foto_bb_ctx* c, double* phi);
+int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3);
+int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc);
+int foto_bb_stats_get(const foto_bb_ctx* c, foto_bb_stats* st);
+int foto_bb_stats_reset(foto_bb_ctx* c);
+/* enable / disable per-launch HIP-event timing (foto_bb_stats.n_k / ms_k) */
+int foto_bb_set_timing(foto_bb_ctx* c, int on);
+int foto_bb_sync(foto_bb_ctx* c);
+void foto_bb_destroy(foto_bb_ctx* c);
+
+/* One-shot benamou_brenier.solve(rho0, rhoT, Nt, Nx, Ny, r, convergence_tol,
+ * reg_epsilon, max_it) -> (u, v, m) on one GPU.                                     */
+int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r,
+                  double convergence_tol, double reg_epsilon, int max_it, foto_bb_iter_cb cb, void* user,
+                  double* u, double* v, double* m);
+
+/* RCCL unique id for foto_bb_opts.nccl_id (call on rank 0, broadcast 128 bytes). */
+int foto_nccl_unique_id(void* out128);
+
+/* ------------------------------------------------------------------ GN baseline
+ * classical.GLLOpticalFlow (classical.py:25-130).                                 */
+/* assemble(f1, f2).A @ x and .b (classical.py:68-111)                             */
+int foto_gn_apply(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
+                  const double* x3, double* y3);
+int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
+/* process(): spsolve replaced by block-Jacobi PCG to rtol (default 1e-10).
+ * Returns 0 (converged) or maxiter (not converged), < 0 on error.                 */
+int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
+                  double rtol, int maxiter, double* u, double* v, double* m, int* iterations);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FOTO_H */

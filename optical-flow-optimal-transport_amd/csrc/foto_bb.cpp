@@ -1,0 +1,725 @@
+// libfoto host side: the Benamou-Brenier solver context, the device-resident CG driver,
+// time-slab sharding (RCCL across processes, or in-process virtual ranks on one device
+// for testing the sharded path), and the BB part of the C ABI (include/foto.h).
+//
+// Reference: benamou_brenier.solve (benamou_brenier.py:151-271).  One outer iteration =
+//   stepA: F = div_st(mu - r q) + BC (k_rhs), phi = cg(A, F) (k_cg_dir / k_cg_upd loop)
+//   stepB: q = Proj_K(grad_st phi + mu / r); stepC: mu += r (grad phi - q), mu_rho >= 0;
+//   crit = sqrt(num / (den + 1e-10))  (all fused in k_prox)
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstddef>
+#include <cstring>
+#include <memory>
+
+#include "foto_internal.h"
+#include "foto_spectral.h"
+
+namespace foto {
+
+static thread_local char g_err[2048] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+#define FOTO_NCCL_CHECK(call)                                                                 \
+    do {                                                                                     \
+        ncclResult_t r_ = (call);                                                            \
+        if (r_ != ncclSuccess) {                                                             \
+            ::foto::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
+            return FOTO_ERR_COMM;                                                            \
+        }                                                                                    \
+    } while (0)
+
+// ----------------------------------------------------------------------------- shards
+
+struct Shard {
+    Geo g{};
+    int rank = 0;
+    // fields: halo-padded planes (l = -1 .. nloc), pointers at local plane 0
+    double* mu[3] = {nullptr, nullptr, nullptr};
+    double* q[3] = {nullptr, nullptr, nullptr};
+    double* phi = nullptr;   // CG iterate x
+    double* rv = nullptr;    // CG residual (starts as F)
+    double* p[2] = {nullptr, nullptr};
+    double* rho0 = nullptr;
+    double* rhoT = nullptr;
+    double* px = nullptr;    // trajectory positions
+    double* py = nullptr;
+    double* fu = nullptr;    // flow output (last rank)
+    double* fv = nullptr;
+    double* fm = nullptr;
+    RedBuf rb{};
+    double* gath = nullptr;  // [0,W) rr | [W,2W) pap | [2W,4W) crit num/den
+    CGScal* S = nullptr;
+    std::vector<void*> allocs;
+    std::unique_ptr<SpectralPlan> spec;
+
+    double* gath_rr() { return gath; }
+    double* gath_pap(int W) { return gath + W; }
+    double* gath_crit(int W) { return gath + 2 * W; }
+
+    int alloc(size_t bytes, void** out) {
+        FOTO_HIP_CHECK(hipMalloc(out, bytes));
+        allocs.push_back(*out);
+        return 0;
+    }
+    int alloc_field(double** out) {   // (nloc + 2) planes, zeroed
+        void* b = nullptr;
+        const size_t n = (size_t)(g.nloc + 2) * (size_t)g.nxy;
+        FOTO_TRY(alloc(n * sizeof(double), &b));
+        FOTO_HIP_CHECK(hipMemset(b, 0, n * sizeof(double)));
+        *out = (double*)b + g.nxy;
+        return 0;
+    }
+    ~Shard() {
+        for (void* a : allocs) (void)hipFree(a);
+    }
+};
+
+static int split_planes(int Nt, int W, int rank, int* t0, int* nloc) {
+    const int base = Nt / W, extra = Nt % W;
+    *nloc = base + (rank < extra ? 1 : 0);
+    *t0 = rank * base + std::min(rank, extra);
+    return *nloc >= 1 ? 0 : -1;
+}
+
+// ----------------------------------------------------------------------------- timing
+
+struct KTimer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    struct Pend { hipEvent_t a, b; int cls; double bytes; };
+    std::vector<Pend> pend;
+    int64_t n[8] = {0};
+    double ms[8] = {0};
+    double bytes[8] = {0};
+
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    // returns the start event to be paired by stop()
+    hipEvent_t start(hipStream_t s) {
+        if (!on) return nullptr;
+        hipEvent_t e = get();
+        if (e) (void)hipEventRecord(e, s);
+        return e;
+    }
+    void stop(hipEvent_t a, hipStream_t s, int cls, double by) {
+        if (!on || !a) return;
+        hipEvent_t b = get();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        pend.push_back({a, b, cls, by});
+    }
+    void resolve() {   // call after a stream sync
+        for (auto& p : pend) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+                n[p.cls] += 1;
+                ms[p.cls] += t;
+                bytes[p.cls] += p.bytes;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pend.clear();
+    }
+    void reset() {
+        std::fill(n, n + 8, 0);
+        std::fill(ms, ms + 8, 0.0);
+        std::fill(bytes, bytes + 8, 0.0);
+    }
+    ~KTimer() {
+        for (auto& p : pend) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+}  // namespace foto
+
+using namespace foto;
+
+// ----------------------------------------------------------------------------- context
+
+struct foto_bb_ctx {
+    int Nt = 0, Nx = 0, Ny = 0;
+    double r = 1, eps = 1e-3;
+    foto_bb_opts o{};
+    int W = 1;            // total ranks (processes * virtual)
+    bool rccl = false;
+    ncclComm_t nc = nullptr;
+    hipStream_t s = nullptr;
+    std::vector<std::unique_ptr<Shard>> sh;   // local shards
+    CGScal* hS = nullptr;                     // pinned host mirror of shard 0's CG scalars
+    double* hgath = nullptr;                  // pinned host mirror of gath
+    int last_cg = 0;
+    int have_phi = 0;
+    // bookkeeping
+    double prev_crit = -1;
+    foto_bb_stats st{};
+    KTimer kt;
+    hipEvent_t ph[2] = {nullptr, nullptr};
+    ~foto_bb_ctx() {
+        sh.clear();
+        if (nc) (void)ncclCommDestroy(nc);
+        if (hS) (void)hipHostFree(hS);
+        if (hgath) (void)hipHostFree(hgath);
+        for (auto e : ph) if (e) (void)hipEventDestroy(e);
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
+
+namespace foto {
+
+// ----------------------------------------------------------------------------- communication
+// Virtual ranks share one stream, so plain device copies keep everything ordered.
+
+template <class Pick>
+static int allgather(foto_bb_ctx* c, Pick pick, int cnt) {
+    if (c->W == 1) return 0;
+    if (c->rccl) {
+        Shard& s = *c->sh[0];
+        double* base = pick(s);
+        FOTO_NCCL_CHECK(ncclAllGather(base + (size_t)s.rank * cnt, base, cnt, ncclDouble, c->nc, c->s));
+        return 0;
+    }
+    for (auto& a : c->sh)
+        for (auto& b : c->sh)
+            if (a.get() != b.get())
+                FOTO_HIP_CHECK(hipMemcpyAsync(pick(*a) + (size_t)b->rank * cnt, pick(*b) + (size_t)b->rank * cnt,
+                                              cnt * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+    return 0;
+}
+
+// halo planes of a halo-padded field: plane -1 <- previous rank's last plane, plane nloc <-
+// next rank's first plane.
+template <class Pick>
+static int halo(foto_bb_ctx* c, Pick pick) {
+    if (c->W == 1) return 0;
+    if (c->rccl) {
+        Shard& s = *c->sh[0];
+        double* a = pick(s);
+        const size_t n = (size_t)s.g.nxy;
+        FOTO_NCCL_CHECK(ncclGroupStart());
+        if (s.rank > 0) {
+            FOTO_NCCL_CHECK(ncclSend(a, n, ncclDouble, s.rank - 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclRecv(a - n, n, ncclDouble, s.rank - 1, c->nc, c->s));
+        }
+        if (s.rank < c->W - 1) {
+            FOTO_NCCL_CHECK(ncclSend(a + (size_t)(s.g.nloc - 1) * n, n, ncclDouble, s.rank + 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclRecv(a + (size_t)s.g.nloc * n, n, ncclDouble, s.rank + 1, c->nc, c->s));
+        }
+        FOTO_NCCL_CHECK(ncclGroupEnd());
+        return 0;
+    }
+    for (size_t j = 0; j + 1 < c->sh.size(); ++j) {
+        Shard& lo = *c->sh[j];
+        Shard& hi = *c->sh[j + 1];
+        const size_t n = (size_t)lo.g.nxy;
+        double* a = pick(lo);
+        double* b = pick(hi);
+        FOTO_HIP_CHECK(hipMemcpyAsync(a + (size_t)lo.g.nloc * n, b, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(b - n, a + (size_t)(lo.g.nloc - 1) * n, n * sizeof(double),
+                                      hipMemcpyDeviceToDevice, c->s));
+    }
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- context setup
+
+static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
+    const int64_t nxy = (int64_t)c->Nx * c->Ny;
+    if (c->o.device >= 0) FOTO_HIP_CHECK(hipSetDevice(c->o.device));
+    FOTO_HIP_CHECK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hS, sizeof(CGScal)));
+    const int W = c->W;
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hgath, sizeof(double) * 4 * W));
+    for (auto& e : c->ph) FOTO_HIP_CHECK(hipEventCreate(&e));
+    if (c->rccl) {
+        ncclUniqueId id;
+        memcpy(&id, c->o.nccl_id, sizeof(id));
+        FOTO_NCCL_CHECK(ncclCommInitRank(&c->nc, W, id, c->o.rank));
+    }
+    const int nlocal = c->rccl ? 1 : W;
+    for (int j = 0; j < nlocal; ++j) {
+        auto sp = std::make_unique<Shard>();
+        Shard& s = *sp;
+        s.rank = c->rccl ? c->o.rank : j;
+        s.g.Nt = c->Nt; s.g.Ny = c->Ny; s.g.Nx = c->Nx; s.g.nxy = nxy;
+        if (split_planes(c->Nt, W, s.rank, &s.g.t0, &s.g.nloc) != 0) {
+            set_error("world size %d exceeds Nt = %d (each rank needs >= 1 time slab)", W, c->Nt);
+            return FOTO_ERR_ARG;
+        }
+        for (int f = 0; f < 3; ++f) { FOTO_TRY(s.alloc_field(&s.mu[f])); FOTO_TRY(s.alloc_field(&s.q[f])); }
+        FOTO_TRY(s.alloc_field(&s.phi));
+        FOTO_TRY(s.alloc_field(&s.rv));
+        FOTO_TRY(s.alloc_field(&s.p[0]));
+        FOTO_TRY(s.alloc_field(&s.p[1]));
+        void* b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.rho0 = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.rhoT = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.px = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.py = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.fu = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.fv = (double*)b;
+        FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.fm = (double*)b;
+        const int64_t nb = std::max<int64_t>(march_blocks(s.g), flat_blocks((int64_t)s.g.nloc * nxy));
+        s.rb.cap = (int)(2 * nb);
+        FOTO_TRY(s.alloc(sizeof(double) * s.rb.cap, &b)); s.rb.partials = (double*)b;
+        FOTO_TRY(s.alloc(sizeof(unsigned) * 64, &b)); s.rb.ticket = (unsigned*)b;
+        FOTO_HIP_CHECK(hipMemset(s.rb.ticket, 0, sizeof(unsigned) * 64));
+        FOTO_TRY(s.alloc(sizeof(double) * 4 * W, &b)); s.gath = (double*)b;
+        FOTO_HIP_CHECK(hipMemset(s.gath, 0, sizeof(double) * 4 * W));
+        FOTO_TRY(s.alloc(sizeof(CGScal), &b)); s.S = (CGScal*)b;
+        FOTO_HIP_CHECK(hipMemcpyAsync(s.rho0, rho0, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(s.rhoT, rhoT, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
+        FOTO_HIP_CHECK(launch_init_mu(s.g, s.rho0, s.rhoT, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->s));
+        if (c->o.cg_mode == 1) {
+            s.spec.reset(new SpectralPlan());
+            FOTO_TRY(s.spec->init(s.g, W, c->r, c->eps, c->s));
+        }
+        c->sh.push_back(std::move(sp));
+    }
+    if (c->o.cg_mode == 1 && W > 1) {
+        set_error("spectral CG (cg_mode=1) is single-shard only in this build");
+        return FOTO_ERR_ARG;
+    }
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- CG driver
+
+static CGArgs cg_args(foto_bb_ctx* c, const Shard& s) {
+    CGArgs a;
+    a.r = c->r;
+    a.eps = c->eps;
+    a.rtol = c->o.cg_rtol;
+    a.world = c->W;
+    a.rank = s.rank;
+    return a;
+}
+
+static int cg_iteration(foto_bb_ctx* c, int k) {
+    const int W = c->W;
+    const bool fused = (W == 1);
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        double* pold = s.p[k & 1];
+        double* pnew = s.p[(k + 1) & 1];
+        const CGArgs a = cg_args(c, s);
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        if (!fused) FOTO_HIP_CHECK(launch_cg_pupd(s.g, k, s.rv, pold, pnew, s.S, s.gath_rr(), a, c->s));
+        (void)nv;
+    }
+    if (!fused) FOTO_TRY(halo(c, [k](Shard& s) { return s.p[(k + 1) & 1]; }));
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const CGArgs a = cg_args(c, s);
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        hipEvent_t e = c->kt.start(c->s);
+        FOTO_HIP_CHECK(launch_cg_dir(s.g, k, s.rv, s.p[k & 1], s.p[(k + 1) & 1], a, s.S, s.rb, s.gath_rr(),
+                                     s.gath_pap(W), fused ? 1 : 0, c->s));
+        c->kt.stop(e, c->s, FOTO_K_CG_DIR, fused ? (k == 0 ? 16.0 : 24.0) * nv : 8.0 * nv);
+    }
+    FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_pap(W); }, 1));
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const CGArgs a = cg_args(c, s);
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        hipEvent_t e = c->kt.start(c->s);
+        FOTO_HIP_CHECK(launch_cg_upd(s.g, k, s.p[(k + 1) & 1], s.phi, s.rv, a, s.S, s.rb, s.gath_pap(W),
+                                     s.gath_rr(), c->s));
+        c->kt.stop(e, c->s, FOTO_K_CG_UPD, (k == 0 ? 32.0 : 40.0) * nv);
+    }
+    FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    return 0;
+}
+
+// Solve A x = F (F already in rv, F.F gathered in gath_rr) to scipy's stopping rule.
+// The loop runs on the device; the host only polls the done flag between chunks.  Every
+// rank takes the same decisions (the flag is a function of gathered scalars), so the
+// collective call sequence stays identical across ranks.
+static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
+    const int maxiter = c->o.cg_maxiter;
+    if (c->o.cg_mode == 1) {
+        Shard& s = *c->sh[0];
+        FOTO_TRY(s.spec->solve(s.rv, s.phi, c->o.cg_rtol, maxiter, c->last_cg, iters, info, &c->kt, c->s));
+        c->last_cg = *iters;
+        return 0;
+    }
+    for (auto& sp : c->sh) FOTO_HIP_CHECK(hipMemsetAsync(sp->S, 0, sizeof(CGScal), c->s));
+    int k = 0;
+    bool done = false;
+    const int first = c->last_cg > 4 ? c->last_cg - 3 : 6;
+    while (k < maxiter) {
+        int chunk = (k == 0) ? first : 2;
+        chunk = std::min(chunk, maxiter - k);
+        for (int j = 0; j < chunk; ++j, ++k) FOTO_TRY(cg_iteration(c, k));
+        FOTO_HIP_CHECK(hipMemcpyAsync(c->hS, c->sh[0]->S, sizeof(CGScal), hipMemcpyDeviceToHost, c->s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+        if (c->hS->done) { done = true; break; }
+    }
+    if (done) {
+        *iters = c->hS->iters;
+        *info = 0;
+        if (*iters == 0)
+            for (auto& sp : c->sh)
+                FOTO_HIP_CHECK(hipMemsetAsync(sp->phi, 0, sizeof(double) * sp->g.nloc * sp->g.nxy, c->s));
+    } else {
+        *iters = maxiter;
+        *info = maxiter;
+    }
+    c->last_cg = *iters;
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- outer iteration
+
+static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_info) {
+    const int W = c->W;
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+    FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
+    FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        hipEvent_t e = c->kt.start(c->s);
+        FOTO_HIP_CHECK(launch_rhs(s.g, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], s.rho0, s.rhoT, c->r,
+                                  s.rv, s.rb, s.gath_rr(), s.rank, c->s));
+        c->kt.stop(e, c->s, FOTO_K_RHS, 56.0 * nv);
+    }
+    FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
+    float t_rhs = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->ph[0], c->ph[1]));
+    c->st.ms_rhs += t_rhs;
+
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+    FOTO_TRY(cg_solve(c, cg_iters, cg_info));
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
+    float t_cg = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[0], c->ph[1]));
+    c->st.ms_cg += t_cg;
+    c->have_phi = 1;
+
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+    FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        hipEvent_t e = c->kt.start(c->s);
+        FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
+                                   s.gath_crit(W), s.rank, c->s));
+        c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+    }
+    FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
+    FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
+    float t_prox = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, c->ph[0], c->ph[1]));
+    c->st.ms_prox += t_prox;
+    c->kt.resolve();
+
+    double num = 0.0, den = 0.0;
+    for (int g = 0; g < W; ++g) { num += c->hgath[2 * W + 2 * g]; den += c->hgath[2 * W + 2 * g + 1]; }
+    *crit = std::sqrt(num / (den + 1e-10));
+    c->st.outer_iters += 1;
+    c->st.cg_iters_total += *cg_iters;
+    c->st.last_crit = *crit;
+    return 0;
+}
+
+static int flow(foto_bb_ctx* c, double* u, double* v, double* m) {
+    if (!c->have_phi) {
+        set_error("foto_bb_flow: no outer iteration has run yet (reference: UnboundLocalError for max_it=0)");
+        return FOTO_ERR_STATE;
+    }
+    const int W = c->W;
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+    if (c->rccl) {
+        Shard& s = *c->sh[0];
+        const size_t n = (size_t)s.g.nxy;
+        if (s.rank > 0) {
+            FOTO_NCCL_CHECK(ncclGroupStart());
+            FOTO_NCCL_CHECK(ncclRecv(s.px, n, ncclDouble, s.rank - 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclRecv(s.py, n, ncclDouble, s.rank - 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclGroupEnd());
+        }
+        const int n_lo = s.g.t0, n_hi = std::min(s.g.t0 + s.g.nloc, c->Nt - 1);
+        FOTO_HIP_CHECK(launch_traj(s.g, s.phi, n_lo, std::max(n_lo, n_hi), s.px, s.py, s.rank == 0, c->s));
+        if (s.rank < W - 1) {
+            FOTO_NCCL_CHECK(ncclGroupStart());
+            FOTO_NCCL_CHECK(ncclSend(s.px, n, ncclDouble, s.rank + 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclSend(s.py, n, ncclDouble, s.rank + 1, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclGroupEnd());
+        } else {
+            FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s.px, s.py, s.fu, s.fv, s.fm, c->s));
+        }
+        // deliver (u, v, m) to rank 0
+        if (W > 1) {
+            FOTO_NCCL_CHECK(ncclGroupStart());
+            if (s.rank == W - 1) {
+                FOTO_NCCL_CHECK(ncclSend(s.fu, n, ncclDouble, 0, c->nc, c->s));
+                FOTO_NCCL_CHECK(ncclSend(s.fv, n, ncclDouble, 0, c->nc, c->s));
+                FOTO_NCCL_CHECK(ncclSend(s.fm, n, ncclDouble, 0, c->nc, c->s));
+            }
+            if (s.rank == 0) {
+                FOTO_NCCL_CHECK(ncclRecv(s.fu, n, ncclDouble, W - 1, c->nc, c->s));
+                FOTO_NCCL_CHECK(ncclRecv(s.fv, n, ncclDouble, W - 1, c->nc, c->s));
+                FOTO_NCCL_CHECK(ncclRecv(s.fm, n, ncclDouble, W - 1, c->nc, c->s));
+            }
+            FOTO_NCCL_CHECK(ncclGroupEnd());
+        }
+        if (s.rank == 0 && u && v && m) {
+            FOTO_HIP_CHECK(hipMemcpyAsync(u, s.fu, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(v, s.fv, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(m, s.fm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        }
+    } else {
+        for (size_t j = 0; j < c->sh.size(); ++j) {
+            Shard& s = *c->sh[j];
+            const size_t n = (size_t)s.g.nxy;
+            if (j > 0) {
+                FOTO_HIP_CHECK(hipMemcpyAsync(s.px, c->sh[j - 1]->px, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+                FOTO_HIP_CHECK(hipMemcpyAsync(s.py, c->sh[j - 1]->py, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+            }
+            const int n_lo = s.g.t0, n_hi = std::min(s.g.t0 + s.g.nloc, c->Nt - 1);
+            FOTO_HIP_CHECK(launch_traj(s.g, s.phi, n_lo, std::max(n_lo, n_hi), s.px, s.py, j == 0, c->s));
+        }
+        Shard& s = *c->sh.back();
+        const size_t n = (size_t)s.g.nxy;
+        FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s.px, s.py, s.fu, s.fv, s.fm, c->s));
+        if (u && v && m) {
+            FOTO_HIP_CHECK(hipMemcpyAsync(u, s.fu, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(v, s.fv, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(m, s.fm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        }
+    }
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
+    float t = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t, c->ph[0], c->ph[1]));
+    c->st.ms_flow += t;
+    return 0;
+}
+
+}  // namespace foto
+
+// ============================================================================ C ABI (BB)
+
+extern "C" {
+
+const char* foto_last_error(void) { return foto::g_err; }
+int foto_version(void) { return 1; }
+
+int foto_device_count(int* n) {
+    FOTO_HIP_CHECK(hipGetDeviceCount(n));
+    return 0;
+}
+
+int foto_bb_opts_default(foto_bb_opts* o) {
+    if (!o) return FOTO_ERR_ARG;
+    memset(o, 0, sizeof(*o));
+    o->device = -1;
+    o->cg_maxiter = 1000;
+    o->cg_rtol = 1e-6;
+    o->cg_mode = 0;
+    o->rank = 0;
+    o->world = 1;
+    o->nccl_id = nullptr;
+    o->virtual_ranks = 1;
+    o->timing = 0;
+    return 0;
+}
+
+int foto_nccl_unique_id(void* out128) {
+    ncclUniqueId id;
+    FOTO_NCCL_CHECK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out128, &id, sizeof(id));
+    return 0;
+}
+
+static int check_grid(int Nt, int Nx, int Ny) {
+    if (Nt < 2) {
+        set_error("Nt = %d: the reference needs Nt >= 2 (benamou_brenier.py:194 divides by Nt-1)", Nt);
+        return FOTO_ERR_ARG;
+    }
+    if (Nx < 2 || Ny < 2) {
+        set_error("Nx = %d, Ny = %d: operators need >= 2 points per axis (operators.py lap1d IndexError)", Nx, Ny);
+        return FOTO_ERR_ARG;
+    }
+    return 0;
+}
+
+int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r, double reg_epsilon,
+                   const foto_bb_opts* opts, foto_bb_ctx** out) {
+    if (!rho0 || !rhoT || !out) { set_error("null argument"); return FOTO_ERR_ARG; }
+    FOTO_TRY(check_grid(Nt, Nx, Ny));
+    foto_bb_opts o;
+    if (opts) o = *opts; else foto_bb_opts_default(&o);
+    if (o.world < 1 || o.rank < 0 || o.rank >= o.world) { set_error("bad rank/world"); return FOTO_ERR_ARG; }
+    if (o.world > 1 && o.virtual_ranks > 1) { set_error("virtual_ranks requires world == 1"); return FOTO_ERR_ARG; }
+    if (o.world > 1 && !o.nccl_id) { set_error("world > 1 needs nccl_id"); return FOTO_ERR_ARG; }
+    if (o.cg_maxiter < 0) { set_error("cg_maxiter < 0"); return FOTO_ERR_ARG; }
+    auto c = std::make_unique<foto_bb_ctx>();
+    c->Nt = Nt; c->Nx = Nx; c->Ny = Ny; c->r = r; c->eps = reg_epsilon; c->o = o;
+    c->rccl = o.world > 1;
+    c->W = c->rccl ? o.world : std::max(1, o.virtual_ranks);
+    c->kt.on = o.timing != 0;
+    int rc = ctx_init(c.get(), rho0, rhoT);
+    if (rc < 0) return rc;
+    *out = c.release();
+    return 0;
+}
+
+int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rules, foto_bb_iter_cb cb, void* user,
+                    int* iters_done) {
+    if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
+    int done = 0;
+    int stopped = 0;
+    for (int i = 0; i < max_iters; ++i) {
+        double crit;
+        int its, info;
+        FOTO_TRY(outer_iteration(c, &crit, &its, &info));
+        ++done;
+        if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
+        const double prev = c->prev_crit;
+        c->prev_crit = crit;
+        if (use_stop_rules) {
+            if (crit <= tol) { stopped = 1; break; }
+            if (prev >= 0 && std::fabs(prev - crit) < 1e-5) { stopped = 1; break; }
+        }
+    }
+    if (iters_done) *iters_done = done;
+    return stopped;
+}
+
+int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m) {
+    if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
+    return flow(c, u, v, m);
+}
+
+int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc) {
+    if (!c) return FOTO_ERR_ARG;
+    if (c->rccl) { *t0 = c->sh[0]->g.t0; *nloc = c->sh[0]->g.nloc; }
+    else { *t0 = 0; *nloc = c->Nt; }
+    return 0;
+}
+
+int foto_bb_get_phi(foto_bb_ctx* c, double* phi) {
+    if (!c || !phi) return FOTO_ERR_ARG;
+    size_t off = 0;
+    for (auto& sp : c->sh) {
+        const size_t n = (size_t)sp->g.nloc * sp->g.nxy;
+        FOTO_HIP_CHECK(hipMemcpyAsync(phi + off, sp->phi, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        off += n;
+    }
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3) {
+    if (!c) return FOTO_ERR_ARG;
+    size_t tot = 0;
+    for (auto& sp : c->sh) tot += (size_t)sp->g.nloc * sp->g.nxy;
+    for (int f = 0; f < 3; ++f) {
+        size_t off = 0;
+        for (auto& sp : c->sh) {
+            const size_t n = (size_t)sp->g.nloc * sp->g.nxy;
+            if (mu3) FOTO_HIP_CHECK(hipMemcpyAsync(mu3 + f * tot + off, sp->mu[f], n * 8, hipMemcpyDeviceToHost, c->s));
+            if (q3) FOTO_HIP_CHECK(hipMemcpyAsync(q3 + f * tot + off, sp->q[f], n * 8, hipMemcpyDeviceToHost, c->s));
+            off += n;
+        }
+    }
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+int foto_bb_stats_get(const foto_bb_ctx* c, foto_bb_stats* st) {
+    if (!c || !st) return FOTO_ERR_ARG;
+    *st = c->st;
+    for (int k = 0; k < 8; ++k) { st->n_k[k] = c->kt.n[k]; st->ms_k[k] = c->kt.ms[k]; st->bytes_k[k] = c->kt.bytes[k]; }
+    return 0;
+}
+
+int foto_bb_stats_reset(foto_bb_ctx* c) {
+    if (!c) return FOTO_ERR_ARG;
+    const int oi = c->st.outer_iters;
+    memset(&c->st, 0, sizeof(c->st));
+    c->st.outer_iters = oi;
+    c->kt.reset();
+    return 0;
+}
+
+int foto_bb_set_timing(foto_bb_ctx* c, int on) {
+    if (!c) return FOTO_ERR_ARG;
+    c->kt.on = on != 0;
+    return 0;
+}
+
+int foto_bb_sync(foto_bb_ctx* c) {
+    if (!c) return FOTO_ERR_ARG;
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+void foto_bb_destroy(foto_bb_ctx* c) { delete c; }
+
+int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r, double tol, double eps,
+                  int max_it, foto_bb_iter_cb cb, void* user, double* u, double* v, double* m) {
+    foto_bb_ctx* c = nullptr;
+    FOTO_TRY(foto_bb_create(rho0, rhoT, Nt, Nx, Ny, r, eps, nullptr, &c));
+    int done = 0;
+    int rc = foto_bb_iterate(c, max_it, tol, 1, cb, user, &done);
+    if (rc >= 0) rc = foto_bb_flow(c, u, v, m);
+    if (rc >= 0) rc = foto_bb_sync(c);
+    foto_bb_destroy(c);
+    return rc < 0 ? rc : 0;
+}
+
+}  // extern "C"
+
+extern "C" int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double eps, double rtol, int maxiter, int mode,
+                       double* x, int* iterations) {
+    if (!b || !x) { set_error("null argument"); return FOTO_ERR_ARG; }
+    FOTO_TRY(check_grid(Nt, Nx, Ny));
+    const int64_t nxy = (int64_t)Nx * Ny, N = nxy * Nt;
+    std::vector<double> z((size_t)nxy, 0.0);
+    foto_bb_opts o;
+    foto_bb_opts_default(&o);
+    o.cg_rtol = rtol;
+    o.cg_maxiter = maxiter;
+    o.cg_mode = mode;
+    foto_bb_ctx* c = nullptr;
+    FOTO_TRY(foto_bb_create(z.data(), z.data(), Nt, Nx, Ny, r, eps, &o, &c));
+    std::unique_ptr<foto_bb_ctx> guard(c);
+    Shard& s = *c->sh[0];
+    FOTO_HIP_CHECK(hipMemcpyAsync(s.rv, b, N * sizeof(double), hipMemcpyHostToDevice, c->s));
+    FOTO_HIP_CHECK(launch_dot_self(N, s.rv, s.rb, s.gath_rr(), 0, c->s));
+    int its = 0, info = 0;
+    FOTO_TRY(cg_solve(c, &its, &info));
+    FOTO_HIP_CHECK(hipMemcpyAsync(x, s.phi, N * sizeof(double), hipMemcpyDeviceToHost, c->s));
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    if (iterations) *iterations = its;
+    return info;
+}
+
+// ctypes mirrors these layouts (foto/_lib.py); tests/test_cabi.py checks the Python side.
+static_assert(sizeof(foto_bb_opts) == 48, "foto_bb_opts layout");
+static_assert(offsetof(foto_bb_stats, n_k) == 56, "foto_bb_stats layout");

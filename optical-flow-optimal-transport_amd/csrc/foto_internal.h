@@ -1,0 +1,131 @@
+// Internal declarations shared by the libfoto translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/foto.h"
+
+namespace foto {
+
+// ----------------------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+
+#define FOTO_HIP_CHECK(call)                                                                  \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            ::foto::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return FOTO_ERR_HIP;                                                             \
+        }                                                                                    \
+    } while (0)
+
+#define FOTO_TRY(expr)          \
+    do {                        \
+        int rc_ = (expr);       \
+        if (rc_ < 0) return rc_; \
+    } while (0)
+
+// ----------------------------------------------------------------------------- geometry
+// One time-slab shard of the (Nt, Ny, Nx) grid: local planes l in [0, nloc) are global
+// planes t0 + l.  Every field array is allocated with one halo plane below (l = -1) and
+// one above (l = nloc); the device pointer handed to kernels points at local plane 0.
+struct Geo {
+    int Nt, Ny, Nx;
+    int t0, nloc;
+    int64_t nxy;
+};
+
+constexpr int TX = 64;   // march tile width  (one wave = one 64-voxel x-row, 512 B of fp64)
+constexpr int TY = 4;    // march tile height (4 waves, 256 threads)
+constexpr int NT = 256;  // threads per block for every kernel
+
+inline int march_blocks(const Geo& g) { return ((g.Nx + TX - 1) / TX) * ((g.Ny + TY - 1) / TY); }
+inline int flat_blocks(int64_t n) { return (int)((n + NT - 1) / NT); }
+
+// Device-side CG scalars (one per shard).  Written only by the last block of a kernel
+// (or by block 0 for the done flag); read by later kernels.
+struct CGScal {
+    double bb;     // b.b
+    double atol;   // rtol * ||b||
+    double rho;    // r_k . r_k of the current iteration (scipy's rho_cur)
+    double pap;    // p_k . A p_k
+    int done;      // converged (top-of-iteration test passed) or b == 0
+    int iters;     // iteration index at which `done` was set
+    int pad[2];
+};
+
+// Per-shard reduction scratch: `partials` holds one value per block per quantity,
+// `ticket` is the last-block counter, `gath` holds one slot per rank (allgathered).
+struct RedBuf {
+    double* partials;
+    unsigned* ticket;
+    int cap;   // blocks * quantities capacity
+};
+
+// ----------------------------------------------------------------------------- kernel launchers
+// (defined in foto_kernels.hip; all enqueue on `s` and never synchronise)
+struct CGArgs {
+    double r, eps, rtol;
+    int world, rank;
+};
+
+hipError_t launch_apply_A(const Geo& g, const double* p, double* out, double r, double eps, int lap_only,
+                          hipStream_t s);
+hipError_t launch_grad_st(const Geo& g, const double* phi, double* gt, double* gx, double* gy, hipStream_t s);
+hipError_t launch_div_st(const Geo& g, const double* wt, const double* wx, const double* wy, double* out,
+                         hipStream_t s);
+hipError_t launch_grad2(int Nx, int Ny, const double* f, double* gx, double* gy, int bcD, hipStream_t s);
+hipError_t launch_div2(int Nx, int Ny, const double* u, const double* v, double* out, int bcD, double sign,
+                       hipStream_t s);
+hipError_t launch_grad2_forward(int Nx, int Ny, const double* f, double* gx, double* gy, hipStream_t s);
+hipError_t launch_stepB(int64_t M, const double* pa, const double* p1, const double* p2, double* qa,
+                        double* q1, double* q2, hipStream_t s);
+hipError_t launch_init_mu(const Geo& g, const double* rho0, const double* rhoT, double* mut, double* mux,
+                          double* muy, double* qt, double* qx, double* qy, hipStream_t s);
+// F = div_st(mu - r q) + BC, written to `F`; F.F partial -> gath[rank]
+hipError_t launch_rhs(const Geo& g, const double* mut, const double* mux, const double* muy, const double* qt,
+                      const double* qx, const double* qy, const double* rho0, const double* rhoT, double r,
+                      double* F, RedBuf rb, double* gath, int rank, hipStream_t s);
+// stencil CG iteration kernels
+hipError_t launch_cg_dir(const Geo& g, int k, const double* rvec, const double* pold, double* pnew,
+                         const CGArgs& a, CGScal* S, RedBuf rb, const double* gath_rr, double* gath_pap,
+                         int fused, hipStream_t s);
+hipError_t launch_cg_pupd(const Geo& g, int k, const double* rvec, const double* pold, double* pnew,
+                          CGScal* S, const double* gath_rr, const CGArgs& a, hipStream_t s);
+hipError_t launch_cg_upd(const Geo& g, int k, const double* p, double* x, double* rvec, const CGArgs& a,
+                         CGScal* S, RedBuf rb, const double* gath_pap, double* gath_rr, hipStream_t s);
+// grad_st phi -> stepB -> mu update -> crit partial sums (num, den) -> gath[2*rank..]
+hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
+                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s);
+// trajectory steps n in [n_lo, n_hi) using phi planes (local plane index l = n - t0)
+hipError_t launch_traj(const Geo& g, const double* phi, int n_lo, int n_hi, double* px, double* py,
+                       int init, hipStream_t s);
+hipError_t launch_flow_finish(int Nx, int Ny, const double* px, const double* py, double* u, double* v,
+                              double* m, hipStream_t s);
+
+hipError_t launch_dot_self(int64_t n, const double* x, RedBuf rb, double* gath, int rank, hipStream_t s);
+
+// GN
+hipError_t launch_gn_coeffs(int w, int h, const double* f1, const double* f2, double* fx, double* fy,
+                            double* ft, hipStream_t s);
+hipError_t launch_gn_rhs(int w, int h, const double* fx, const double* fy, const double* f2, const double* ft,
+                         double* b, hipStream_t s);
+hipError_t launch_gn_apply(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
+                           double lam, const double* x, double* y, hipStream_t s);
+hipError_t launch_gn_pcg_init(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
+                              double lam, const double* b, double* r, double* z, RedBuf rb, double* gath,
+                              hipStream_t s);
+hipError_t launch_gn_pcg_dir(int w, int h, int k, const double* fx, const double* fy, const double* f2,
+                             double alpha, double lam, const double* z, const double* pold, double* pnew,
+                             CGScal* S, RedBuf rb, const double* gath_rz, double* gath_pq, double rtol,
+                             hipStream_t s);
+hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double* fy, const double* f2,
+                             double alpha, double lam, const double* p, double* x, double* r, double* z,
+                             CGScal* S, RedBuf rb, const double* gath_pq, double* gath_rz, hipStream_t s);
+
+}  // namespace foto

@@ -1,0 +1,710 @@
+// libfoto HIP kernels for the Benamou-Brenier (FOTO) hot path -- gfx950 / CDNA4.
+//
+// All arithmetic is float64 and is written in the operation order numpy/scipy use
+// in the reference (the library is built with -ffp-contract=off: numpy and scipy's
+// sparsetools never fuse a*b+c), so every per-voxel result is the reference's bit for
+// bit; only global sums (dot products, crit sums) are reduced in a different -- fixed,
+// deterministic -- order.
+//
+// Layout (reference operators.py:124-126): voxel k = n*Nx*Ny + j*Nx + i.  A shard owns
+// planes [t0, t0+nloc); arrays carry one halo plane on each side (local l = -1, nloc).
+//
+// Hot kernels (stencil CG, one per CG iteration each):
+//   k_cg_dir : p = r + beta p (fused), A p with a 64x4 LDS tile + 1-voxel halo, marching
+//              along t with the t-neighbours in registers; p.Ap block partials.
+//   k_cg_upd : x += alpha p, r -= alpha A p (A p recomputed from p: cheaper than storing
+//              and re-reading q), r.r partials.
+// Both finish with a last-block reduction (write-through partials + agent-scope ticket,
+// MI355X_MICROARCH.md "Valid forms" row 1): no extra launch per dot product.
+#include "foto_internal.h"
+
+namespace foto {
+
+// ============================================================================ reductions
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;
+}
+
+// Fixed-tree block sum of K values; result valid in thread 0.  `sh` holds K*NT/64 doubles.
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        v[k] = wave_sum(v[k]);
+        if (lane == 0) sh[k * (NT / 64) + w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double s = sh[k * (NT / 64)];
+#pragma unroll
+            for (int j = 1; j < NT / 64; ++j) s += sh[k * (NT / 64) + j];
+            v[k] = s;
+        }
+    }
+}
+
+// Every block contributes v[K]; the block whose ticket add comes last sums all block
+// partials in block order (deterministic) and returns true with the totals in thread 0.
+// Hand-off: partials stored sc1 (write-through) + vmcnt(0) before an agent-scope ticket
+// add; the last block reads them with sc1 loads after its add returned and a barrier.
+template <int K>
+__device__ bool grid_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
+    __shared__ double sh[K * (NT / 64)];
+    __shared__ int is_last;
+    block_sum<K>(v, sh);
+    const int nb = gridDim.x;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            __hip_atomic_store(&rb.partials[(int64_t)k * nb + blockIdx.x], v[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(rb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (t == (unsigned)(nb - 1));
+    }
+    __syncthreads();
+    if (!is_last) return false;
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < nb; i += NT) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            acc[k] += __hip_atomic_load(&rb.partials[(int64_t)k * nb + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    block_sum<K>(acc, sh);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) tot[k] = acc[k];
+        __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
+// ============================================================================ stencils
+
+// One row of the space-time operator A = -r L_st + r eps I (benamou_brenier.py:202-203,
+// operators.py:144-157) in scipy's CSR column order: t-1, y-1, x-1, diag, x+1, y+1, t+1.
+// diag = fl(fl(r*c) + fl(r*eps)) with c = number of existing axis neighbours.
+__device__ __forceinline__ double row_A(const Geo& g, int t, int y, int x, double c, double xm, double xp,
+                                        double ym, double yp, double tm, double tp, double r, double reps) {
+    const bool ht = t > 0, hT = t < g.Nt - 1, hy = y > 0, hY = y < g.Ny - 1, hx = x > 0, hX = x < g.Nx - 1;
+    const double cnt = (double)((int)ht + (int)hT + (int)hy + (int)hY + (int)hx + (int)hX);
+    const double mr = -r;
+    const double dg = r * cnt + reps;
+    double s = 0.0;
+    if (ht) s += mr * tm;
+    if (hy) s += mr * ym;
+    if (hx) s += mr * xm;
+    s += dg * c;
+    if (hX) s += mr * xp;
+    if (hY) s += mr * yp;
+    if (hT) s += mr * tp;
+    return s;
+}
+
+// L_st row (entries 1 off-diagonal, -c on the diagonal), same column order.
+__device__ __forceinline__ double row_L(const Geo& g, int t, int y, int x, double c, double xm, double xp,
+                                        double ym, double yp, double tm, double tp) {
+    const bool ht = t > 0, hT = t < g.Nt - 1, hy = y > 0, hY = y < g.Ny - 1, hx = x > 0, hX = x < g.Nx - 1;
+    const double cnt = (double)((int)ht + (int)hT + (int)hy + (int)hY + (int)hx + (int)hX);
+    double s = 0.0;
+    if (ht) s += tm;
+    if (hy) s += ym;
+    if (hx) s += xm;
+    s += (-cnt) * c;
+    if (hX) s += xp;
+    if (hY) s += yp;
+    if (hT) s += tp;
+    return s;
+}
+
+// 2.5-D march over a 64 x TY xy tile: every thread owns one (x, y) column and walks the
+// shard's planes, keeping planes t-1, t, t+1 of its column in registers.  The x/y
+// neighbours of plane t come from a double-buffered LDS tile with a 1-voxel halo (one
+// barrier per plane).  Loads run one plane ahead of use.
+//   val(l, off)  -> field value at local plane l, in-plane offset off (in-domain only)
+//   body(l, t, off, x, y, c, xm, xp, ym, yp, tm, tp)   for in-domain voxels
+template <class Val, class Body>
+__device__ __forceinline__ void march(const Geo& g, int tile, Val val, Body body) {
+    constexpr int LW = TX + 2, LP = (TY + 2) * LW;
+    __shared__ double lds[2 * LP];
+    const int ntx = (g.Nx + TX - 1) / TX;
+    const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * TY;
+    const int tid = threadIdx.x, tx = tid & (TX - 1), ty = tid / TX;
+    const int x = x0 + tx, y = y0 + ty;
+    const bool in = (x < g.Nx) && (y < g.Ny);
+    const int64_t off = in ? (int64_t)y * g.Nx + x : 0;
+    // halo cell owned by this thread (rows above/below by threads 0..127, columns by 128..135)
+    int hx = -1, hy = -1, hl = -1;
+    if (tid < TX) { hx = x0 + tid; hy = y0 - 1; hl = tid + 1; }
+    else if (tid < 2 * TX) { hx = x0 + tid - TX; hy = y0 + TY; hl = (TY + 1) * LW + (tid - TX) + 1; }
+    else if (tid < 2 * TX + TY) { hx = x0 - 1; hy = y0 + (tid - 2 * TX); hl = (tid - 2 * TX + 1) * LW; }
+    else if (tid < 2 * TX + 2 * TY) { hx = x0 + TX; hy = y0 + (tid - 2 * TX - TY); hl = (tid - 2 * TX - TY + 1) * LW + TX + 1; }
+    const bool hv = hl >= 0 && hx >= 0 && hx < g.Nx && hy >= 0 && hy < g.Ny;
+    const int64_t hoff = hv ? (int64_t)hy * g.Nx + hx : 0;
+    const int ci = (ty + 1) * LW + tx + 1;
+    const bool has_lo = g.t0 > 0, has_hi = g.t0 + g.nloc < g.Nt;
+
+    double cm = 0.0, cc = 0.0, cn = 0.0, hc = 0.0;
+    if (in) {
+        if (has_lo) cm = val(-1, off);
+        cc = val(0, off);
+        if (g.nloc > 1 || has_hi) cn = val(1, off);
+    }
+    if (hv) hc = val(0, hoff);
+    for (int l = 0; l < g.nloc; ++l) {
+        double* buf = lds + (l & 1) * LP;
+        buf[ci] = cc;
+        if (hl >= 0) buf[hl] = hc;
+        double cnn = 0.0, hnn = 0.0;
+        if (in && (l + 2 < g.nloc || (l + 2 == g.nloc && has_hi))) cnn = val(l + 2, off);
+        if (hv && l + 1 < g.nloc) hnn = val(l + 1, hoff);
+        __syncthreads();
+        if (in) {
+            body(l, g.t0 + l, off, x, y, cc, buf[ci - 1], buf[ci + 1], buf[ci - LW], buf[ci + LW], cm, cn);
+        }
+        cm = cc;
+        cc = cn;
+        cn = cnn;
+        hc = hnn;
+    }
+}
+
+// ----------------------------------------------------------------------------- apply A / L
+
+__global__ __launch_bounds__(NT) void k_apply_A(Geo g, const double* __restrict__ p, double* __restrict__ out,
+                                                double r, double reps, int lap_only) {
+    const int64_t nxy = g.nxy;
+    march(g, blockIdx.x, [&](int l, int64_t off) { return p[l * nxy + off]; },
+          [&](int l, int t, int64_t off, int x, int y, double c, double xm, double xp, double ym, double yp,
+              double tm, double tp) {
+              out[l * nxy + off] = lap_only ? row_L(g, t, y, x, c, xm, xp, ym, yp, tm, tp)
+                                            : row_A(g, t, y, x, c, xm, xp, ym, yp, tm, tp, r, reps);
+          });
+}
+
+hipError_t launch_apply_A(const Geo& g, const double* p, double* out, double r, double eps, int lap_only,
+                          hipStream_t s) {
+    k_apply_A<<<march_blocks(g), NT, 0, s>>>(g, p, out, r, r * eps, lap_only);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- CG iteration
+
+struct CGPro {
+    bool go;
+    double rr, atol, beta;
+};
+
+// Top of scipy's cg loop for iteration k: rr = r_k . r_k (sum of the per-rank slots, rank
+// order), atol = rtol*||b|| (k = 0: rr = b.b), stop if ||r|| < atol; beta = rr / rho_prev.
+__device__ __forceinline__ CGPro cg_prologue(int k, const CGScal* S, const double* gath_rr, const CGArgs& a,
+                                             CGScal* Sw) {
+    CGPro P;
+    P.go = false;
+    P.beta = 0.0;
+    if (S->done) return P;
+    double rr = 0.0;
+    for (int i = 0; i < a.world; ++i) rr += gath_rr[i];
+    P.rr = rr;
+    if (k == 0) {
+        P.atol = fmax(0.0, a.rtol * sqrt(rr));
+        if (rr == 0.0) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) { Sw->done = 1; Sw->iters = 0; }
+            return P;
+        }
+    } else {
+        P.atol = S->atol;
+    }
+    if (sqrt(rr) < P.atol) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { Sw->done = 1; Sw->iters = k; }
+        return P;
+    }
+    P.beta = (k > 0) ? rr / S->rho : 0.0;
+    P.go = true;
+    return P;
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(NT) void k_cg_dir(Geo g, int k, const double* __restrict__ rv,
+                                               const double* __restrict__ po, double* __restrict__ pn, CGArgs a,
+                                               CGScal* S, RedBuf rb, const double* __restrict__ gath_rr,
+                                               double* __restrict__ gath_pap) {
+    const CGPro P = cg_prologue(k, S, gath_rr, a, S);
+    if (!P.go) return;
+    const int64_t nxy = g.nxy;
+    const double beta = P.beta, r = a.r, reps = a.r * a.eps;
+    double acc = 0.0;
+    march(
+        g, blockIdx.x,
+        [&](int l, int64_t off) -> double {
+            const int64_t i = l * nxy + off;
+            if (!FUSED) return pn[i];
+            if (k == 0) return rv[i];
+            return beta * po[i] + rv[i];   // scipy: p *= beta; p += z
+        },
+        [&](int l, int t, int64_t off, int x, int y, double c, double xm, double xp, double ym, double yp,
+            double tm, double tp) {
+            const double q = row_A(g, t, y, x, c, xm, xp, ym, yp, tm, tp, r, reps);
+            acc += c * q;
+            if (FUSED) pn[l * nxy + off] = c;
+        });
+    double v[1] = {acc}, tot[1];
+    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) {
+        S->rho = P.rr;
+        if (k == 0) { S->bb = P.rr; S->atol = P.atol; }
+        S->pap = tot[0];
+        gath_pap[a.rank] = tot[0];
+    }
+}
+
+// Pointwise p = r + beta p for the sharded (non-fused) path: the halo planes of the new p
+// are then exchanged before k_cg_dir<false> applies A.
+__global__ __launch_bounds__(NT) void k_cg_pupd(Geo g, int k, const double* __restrict__ rv,
+                                                const double* __restrict__ po, double* __restrict__ pn,
+                                                CGScal* S, const double* __restrict__ gath_rr, CGArgs a) {
+    // decision only (no state writes: k_cg_dir<false> repeats the prologue and writes)
+    if (S->done) return;
+    double rr = 0.0;
+    for (int i = 0; i < a.world; ++i) rr += gath_rr[i];
+    double atol = (k == 0) ? fmax(0.0, a.rtol * sqrt(rr)) : S->atol;
+    if (rr == 0.0 || sqrt(rr) < atol) return;
+    const double beta = (k > 0) ? rr / S->rho : 0.0;
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+        pn[i] = (k == 0) ? rv[i] : beta * po[i] + rv[i];
+}
+
+__global__ __launch_bounds__(NT) void k_cg_upd(Geo g, int k, const double* __restrict__ p, double* __restrict__ xv,
+                                               double* __restrict__ rv, CGArgs a, CGScal* S, RedBuf rb,
+                                               const double* __restrict__ gath_pap, double* __restrict__ gath_rr) {
+    if (S->done) return;
+    double pap = 0.0;
+    for (int i = 0; i < a.world; ++i) pap += gath_pap[i];
+    const double alpha = S->rho / pap;
+    const int64_t nxy = g.nxy;
+    const double r = a.r, reps = a.r * a.eps;
+    double acc = 0.0;
+    march(
+        g, blockIdx.x, [&](int l, int64_t off) -> double { return p[l * nxy + off]; },
+        [&](int l, int t, int64_t off, int x, int y, double c, double xm, double xp, double ym, double yp,
+            double tm, double tp) {
+            const double q = row_A(g, t, y, x, c, xm, xp, ym, yp, tm, tp, r, reps);
+            const int64_t i = l * nxy + off;
+            const double ap = alpha * c;
+            xv[i] = (k == 0) ? 0.0 + ap : xv[i] + ap;   // x += alpha*p
+            const double rn = rv[i] - alpha * q;       // r -= alpha*q
+            rv[i] = rn;
+            acc += rn * rn;
+        });
+    double v[1] = {acc}, tot[1];
+    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rr[a.rank] = tot[0];
+}
+
+hipError_t launch_cg_dir(const Geo& g, int k, const double* rvec, const double* pold, double* pnew,
+                         const CGArgs& a, CGScal* S, RedBuf rb, const double* gath_rr, double* gath_pap,
+                         int fused, hipStream_t s) {
+    if (fused)
+        k_cg_dir<true><<<march_blocks(g), NT, 0, s>>>(g, k, rvec, pold, pnew, a, S, rb, gath_rr, gath_pap);
+    else
+        k_cg_dir<false><<<march_blocks(g), NT, 0, s>>>(g, k, rvec, pold, pnew, a, S, rb, gath_rr, gath_pap);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_pupd(const Geo& g, int k, const double* rvec, const double* pold, double* pnew, CGScal* S,
+                          const double* gath_rr, const CGArgs& a, hipStream_t s) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    int nb = (int)std::min<int64_t>((n + NT - 1) / NT, 4096);
+    k_cg_pupd<<<nb, NT, 0, s>>>(g, k, rvec, pold, pnew, S, gath_rr, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_upd(const Geo& g, int k, const double* p, double* x, double* rvec, const CGArgs& a,
+                         CGScal* S, RedBuf rb, const double* gath_pap, double* gath_rr, hipStream_t s) {
+    k_cg_upd<<<march_blocks(g), NT, 0, s>>>(g, k, p, x, rvec, a, S, rb, gath_pap, gath_rr);
+    return hipGetLastError();
+}
+
+// ============================================================================ gradients / divergence
+
+// grad_1d_central_weird (bc 'N', h = 1) row at index k of an axis of length n, given the
+// values at k-1, k, k+1 (operators.py:33-48).  (-0.5 a) + (0.5 b) == 0.5 (b - a) exactly.
+__device__ __forceinline__ double d1w(int k, int n, double m, double c, double p) {
+    if (k == 0) return p - c;
+    if (k == n - 1) return c - m;
+    return 0.5 * (p - m);
+}
+
+__global__ __launch_bounds__(NT) void k_grad_st(Geo g, const double* __restrict__ phi, double* __restrict__ gt,
+                                                double* __restrict__ gx, double* __restrict__ gy) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int l = (int)(i / g.nxy);
+    const int64_t off = i - (int64_t)l * g.nxy;
+    const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + l;
+    const double c = phi[i];
+    gt[i] = d1w(t, g.Nt, t > 0 ? phi[i - g.nxy] : 0.0, c, t < g.Nt - 1 ? phi[i + g.nxy] : 0.0);
+    gx[i] = d1w(x, g.Nx, x > 0 ? phi[i - 1] : 0.0, c, x < g.Nx - 1 ? phi[i + 1] : 0.0);
+    gy[i] = d1w(y, g.Ny, y > 0 ? phi[i - g.Nx] : 0.0, c, y < g.Ny - 1 ? phi[i + g.Nx] : 0.0);
+}
+
+hipError_t launch_grad_st(const Geo& g, const double* phi, double* gt, double* gx, double* gy, hipStream_t s) {
+    k_grad_st<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, phi, gt, gx, gy);
+    return hipGetLastError();
+}
+
+// div_st row (operators.py:129-142): scipy's COO matvec accumulates the t-block terms, then
+// the x-block, then the y-block, each in ascending column order, starting from 0.
+__device__ __forceinline__ void acc_d1w(double& s, int k, int n, double m, double c, double p) {
+    if (k == 0) { s += -1.0 * c; s += 1.0 * p; }
+    else if (k == n - 1) { s += -1.0 * m; s += 1.0 * c; }
+    else { s += -0.5 * m; s += 0.5 * p; }
+}
+
+template <class W>
+__device__ __forceinline__ double div_st_row(const Geo& g, int64_t i, int t, int y, int x, W w) {
+    double s = 0.0;
+    acc_d1w(s, t, g.Nt, t > 0 ? w(0, i - g.nxy) : 0.0, w(0, i), t < g.Nt - 1 ? w(0, i + g.nxy) : 0.0);
+    acc_d1w(s, x, g.Nx, x > 0 ? w(1, i - 1) : 0.0, w(1, i), x < g.Nx - 1 ? w(1, i + 1) : 0.0);
+    acc_d1w(s, y, g.Ny, y > 0 ? w(2, i - g.Nx) : 0.0, w(2, i), y < g.Ny - 1 ? w(2, i + g.Nx) : 0.0);
+    return s;
+}
+
+__global__ __launch_bounds__(NT) void k_div_st(Geo g, const double* __restrict__ wt, const double* __restrict__ wx,
+                                               const double* __restrict__ wy, double* __restrict__ out) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int l = (int)(i / g.nxy);
+    const int64_t off = i - (int64_t)l * g.nxy;
+    const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx);
+    const double* W[3] = {wt, wx, wy};
+    out[i] = div_st_row(g, i, g.t0 + l, y, x, [&](int f, int64_t j) { return W[f][j]; });
+}
+
+hipError_t launch_div_st(const Geo& g, const double* wt, const double* wx, const double* wy, double* out,
+                         hipStream_t s) {
+    k_div_st<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, wt, wx, wy, out);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- RHS (stepA)
+
+// F = div_st(mu - r q); F[t=0] -= rho0 - rho[0] + r a[0]; F[t=Nt-1] += rhoT - rho + r a
+// (benamou_brenier.py:64-82, dt = 1).  F.F partial -> gath[rank] (= b.b for CG).
+__global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mut, const double* __restrict__ mux,
+                                            const double* __restrict__ muy, const double* __restrict__ qt,
+                                            const double* __restrict__ qx, const double* __restrict__ qy,
+                                            const double* __restrict__ rho0, const double* __restrict__ rhoT,
+                                            double r, double* __restrict__ F, RedBuf rb, double* gath, int rank) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double ff = 0.0;
+    if (i < n) {
+        const int l = (int)(i / g.nxy);
+        const int64_t off = i - (int64_t)l * g.nxy;
+        const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + l;
+        const double* M[3] = {mut, mux, muy};
+        const double* Q[3] = {qt, qx, qy};
+        double s = div_st_row(g, i, t, y, x, [&](int f, int64_t j) { return M[f][j] - r * Q[f][j]; });
+        if (t == 0) s -= (rho0[off] - mut[i]) + r * qt[i];
+        if (t == g.Nt - 1) s += (rhoT[off] - mut[i]) + r * qt[i];
+        F[i] = s;
+        ff = s * s;
+    }
+    double v[1] = {ff}, tot[1];
+    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
+}
+
+hipError_t launch_rhs(const Geo& g, const double* mut, const double* mux, const double* muy, const double* qt,
+                      const double* qx, const double* qy, const double* rho0, const double* rhoT, double r,
+                      double* F, RedBuf rb, double* gath, int rank, hipStream_t s) {
+    k_rhs<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb,
+                                                              gath, rank);
+    return hipGetLastError();
+}
+
+// mu_rho[n] = (1 - n/(Nt-1)) rho0 + (n/(Nt-1)) rhoT, m = 0, q = 0 (benamou_brenier.py:191-194)
+__global__ __launch_bounds__(NT) void k_init_mu(Geo g, const double* __restrict__ rho0,
+                                                const double* __restrict__ rhoT, double* mut, double* mux,
+                                                double* muy, double* qt, double* qx, double* qy) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int l = (int)(i / g.nxy);
+    const int64_t off = i - (int64_t)l * g.nxy;
+    const double s = (double)(g.t0 + l) / (double)(g.Nt - 1);
+    mut[i] = (1.0 - s) * rho0[off] + s * rhoT[off];
+    mux[i] = 0.0;
+    muy[i] = 0.0;
+    qt[i] = 0.0;
+    qx[i] = 0.0;
+    qy[i] = 0.0;
+}
+
+hipError_t launch_init_mu(const Geo& g, const double* rho0, const double* rhoT, double* mut, double* mux,
+                          double* muy, double* qt, double* qx, double* qy, hipStream_t s) {
+    k_init_mu<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, rho0, rhoT, mut, mux, muy, qt, qx, qy);
+    return hipGetLastError();
+}
+
+// ============================================================================ stepB (A8)
+
+// Exact formulas and operation order of benamou_brenier.py:123-148 (glibc-pow constants
+// precomputed: (3/2)^(3/2) and the folded Python constants).
+__device__ __forceinline__ void project_K(double al, double b1, double b2, double& oa, double& o1, double& o2) {
+    if (2.0 * al + b1 * b1 + b2 * b2 <= 0.0) {
+        oa = al; o1 = b1; o2 = b2;
+        return;
+    }
+    const double SQRT2 = 1.4142135623730951;
+    const double rho = sqrt(b1 * b1 + b2 * b2);
+    const double th = atan2(b2, b1);
+    const double ap1 = al + 1.0;
+    double aH, rH;
+    if (-32.0 * pow(ap1, 3.0) - 108.0 * (rho * rho) < 0.0) {
+        const double S = 0.3535533905932738 * rho +
+                         0.16666666666666666 * sqrt(1.3333333333333333 * pow(al, 3.0) + 4.0 * (al * al) +
+                                                    4.5 * (rho * rho) + 4.0 * al + 1.3333333333333333);
+        const double c = pow(S, 0.3333333333333333);
+        const double zh = (-0.3333333333333333 * ap1) / c + c;
+        aH = -(zh * zh);
+        rH = SQRT2 * zh;
+    } else {
+        const double m = -al - 1.0;
+        const double zh = 1.632993161855452 * sqrt(m) *
+                          cos(0.3333333333333333 * acos(1.8371173070873836 * rho / pow(m, 1.5)));
+        aH = -0.5 * (zh * zh);
+        rH = zh;
+    }
+    oa = aH;
+    o1 = rH * cos(th);
+    o2 = rH * sin(th);
+}
+
+__global__ __launch_bounds__(NT) void k_stepB(int64_t M, const double* __restrict__ pa, const double* __restrict__ p1,
+                                              const double* __restrict__ p2, double* __restrict__ qa,
+                                              double* __restrict__ q1, double* __restrict__ q2) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= M) return;
+    double a, b, c;
+    project_K(pa[i], p1[i], p2[i], a, b, c);
+    qa[i] = a;
+    q1[i] = b;
+    q2[i] = c;
+}
+
+hipError_t launch_stepB(int64_t M, const double* pa, const double* p1, const double* p2, double* qa, double* q1,
+                        double* q2, hipStream_t s) {
+    k_stepB<<<flat_blocks(M), NT, 0, s>>>(M, pa, p1, p2, qa, q1, q2);
+    return hipGetLastError();
+}
+
+// ============================================================================ stepB + stepC + crit (fused)
+
+// g = grad_st phi; q = Proj_K(g + (1/r) mu); mu += r (g - q); mu_rho = max(mu_rho, 0);
+// num += mu_rho |g_t + (g_x^2 + g_y^2)/2|, den += mu_rho (g_x^2 + g_y^2)
+// (benamou_brenier.py:213-248).
+__global__ __launch_bounds__(NT) void k_prox(Geo g, const double* __restrict__ phi, double* __restrict__ mut,
+                                             double* __restrict__ mux, double* __restrict__ muy,
+                                             double* __restrict__ qt, double* __restrict__ qx,
+                                             double* __restrict__ qy, double r, double inv_r, RedBuf rb,
+                                             double* gath, int rank) {
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double num = 0.0, den = 0.0;
+    if (i < n) {
+        const int l = (int)(i / g.nxy);
+        const int64_t off = i - (int64_t)l * g.nxy;
+        const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + l;
+        const double c = phi[i];
+        const double gt = d1w(t, g.Nt, t > 0 ? phi[i - g.nxy] : 0.0, c, t < g.Nt - 1 ? phi[i + g.nxy] : 0.0);
+        const double gx = d1w(x, g.Nx, x > 0 ? phi[i - 1] : 0.0, c, x < g.Nx - 1 ? phi[i + 1] : 0.0);
+        const double gy = d1w(y, g.Ny, y > 0 ? phi[i - g.Nx] : 0.0, c, y < g.Ny - 1 ? phi[i + g.Nx] : 0.0);
+        const double m0 = mut[i], m1 = mux[i], m2 = muy[i];
+        double a, b1, b2;
+        project_K(gt + inv_r * m0, gx + inv_r * m1, gy + inv_r * m2, a, b1, b2);
+        qt[i] = a;
+        qx[i] = b1;
+        qy[i] = b2;
+        double n0 = m0 + r * (gt - a);
+        n0 = (n0 < 0.0) ? 0.0 : n0;   // np.maximum(mu, 0) (NaN propagates)
+        mut[i] = n0;
+        mux[i] = m1 + r * (gx - b1);
+        muy[i] = m2 + r * (gy - b2);
+        const double gg = gx * gx + gy * gy;
+        num = n0 * fabs(gt + 0.5 * gg);
+        den = n0 * gg;
+    }
+    double v[2] = {num, den}, tot[2];
+    if (grid_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) {
+        gath[2 * rank] = tot[0];
+        gath[2 * rank + 1] = tot[1];
+    }
+}
+
+hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
+                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s) {
+    k_prox<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, r, 1.0 / r, rb,
+                                                               gath, rank);
+    return hipGetLastError();
+}
+
+// ============================================================================ 2-D operators
+
+// grad_1d_central (operators.py:52-65): bc 'N' end rows zero; bc 'D' zero extension.
+__device__ __forceinline__ double d1c(int k, int n, double m, double p, int bcD) {
+    if (k == 0) return bcD ? 0.5 * p : 0.0;
+    if (k == n - 1) return bcD ? -0.5 * m : 0.0;
+    return 0.5 * (p - m);
+}
+
+__global__ __launch_bounds__(NT) void k_grad2(int Nx, int Ny, const double* __restrict__ f, double* __restrict__ gx,
+                                              double* __restrict__ gy, int bcD) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= (int64_t)Nx * Ny) return;
+    const int y = (int)(i / Nx), x = (int)(i - (int64_t)y * Nx);
+    gx[i] = d1c(x, Nx, x > 0 ? f[i - 1] : 0.0, x < Nx - 1 ? f[i + 1] : 0.0, bcD);
+    gy[i] = d1c(y, Ny, y > 0 ? f[i - Nx] : 0.0, y < Ny - 1 ? f[i + Nx] : 0.0, bcD);
+}
+
+hipError_t launch_grad2(int Nx, int Ny, const double* f, double* gx, double* gy, int bcD, hipStream_t s) {
+    k_grad2<<<flat_blocks((int64_t)Nx * Ny), NT, 0, s>>>(Nx, Ny, f, gx, gy, bcD);
+    return hipGetLastError();
+}
+
+// operators.div (operators.py:182-191) row, COO order: x-block terms then y-block terms.
+__device__ __forceinline__ void acc_d1c(double& s, int k, int n, double m, double p, int bcD) {
+    if (k == 0) { if (bcD) s += 0.5 * p; }
+    else if (k == n - 1) { if (bcD) s += -0.5 * m; }
+    else { s += -0.5 * m; s += 0.5 * p; }
+}
+
+__global__ __launch_bounds__(NT) void k_div2(int Nx, int Ny, const double* __restrict__ u, const double* __restrict__ v,
+                                             double* __restrict__ out, int bcD, double sign) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= (int64_t)Nx * Ny) return;
+    const int y = (int)(i / Nx), x = (int)(i - (int64_t)y * Nx);
+    double s = 0.0;
+    acc_d1c(s, x, Nx, x > 0 ? u[i - 1] : 0.0, x < Nx - 1 ? u[i + 1] : 0.0, bcD);
+    acc_d1c(s, y, Ny, y > 0 ? v[i - Nx] : 0.0, y < Ny - 1 ? v[i + Nx] : 0.0, bcD);
+    out[i] = sign * s;
+}
+
+hipError_t launch_div2(int Nx, int Ny, const double* u, const double* v, double* out, int bcD, double sign,
+                       hipStream_t s) {
+    k_div2<<<flat_blocks((int64_t)Nx * Ny), NT, 0, s>>>(Nx, Ny, u, v, out, bcD, sign);
+    return hipGetLastError();
+}
+
+// grad_forward bc 'N' (operators.py:67-79, 171-180): z[k+1] - z[k], last row 0.
+__global__ __launch_bounds__(NT) void k_grad2_fwd(int Nx, int Ny, const double* __restrict__ f,
+                                                  double* __restrict__ gx, double* __restrict__ gy) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= (int64_t)Nx * Ny) return;
+    const int y = (int)(i / Nx), x = (int)(i - (int64_t)y * Nx);
+    gx[i] = (x < Nx - 1) ? -1.0 * f[i] + 1.0 * f[i + 1] : 0.0;
+    gy[i] = (y < Ny - 1) ? -1.0 * f[i] + 1.0 * f[i + Nx] : 0.0;
+}
+
+hipError_t launch_grad2_forward(int Nx, int Ny, const double* f, double* gx, double* gy, hipStream_t s) {
+    k_grad2_fwd<<<flat_blocks((int64_t)Nx * Ny), NT, 0, s>>>(Nx, Ny, f, gx, gy);
+    return hipGetLastError();
+}
+
+// ============================================================================ flow extraction (A13/A14)
+
+// un[n] = G_x phi_n, vn[n] = G_y phi_n (bc 'N': zero on the edge columns / rows).
+__device__ __forceinline__ double un_at(const double* P, int Nx, int yy, int xx) {
+    if (xx == 0 || xx == Nx - 1) return 0.0;
+    return 0.5 * (P[(int64_t)yy * Nx + xx + 1] - P[(int64_t)yy * Nx + xx - 1]);
+}
+__device__ __forceinline__ double vn_at(const double* P, int Nx, int Ny, int yy, int xx) {
+    if (yy == 0 || yy == Ny - 1) return 0.0;
+    return 0.5 * (P[(int64_t)(yy + 1) * Nx + xx] - P[(int64_t)(yy - 1) * Nx + xx]);
+}
+
+__device__ __forceinline__ int trunc_clamp(double v, int hi) {
+    double t = trunc(v);               // int() truncates toward zero
+    if (!(t >= 0.0)) t = 0.0;          // also maps NaN to 0
+    if (t > (double)hi) t = (double)hi;
+    return (int)t;
+}
+
+// reconstructTrajectory (utils.py:44-99) for steps n in [n_lo, n_hi), one thread per pixel.
+__global__ __launch_bounds__(NT) void k_traj(Geo g, const double* __restrict__ phi, int n_lo, int n_hi,
+                                             double* __restrict__ px, double* __restrict__ py, int init) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= g.nxy) return;
+    const int Nx = g.Nx, Ny = g.Ny;
+    const int j = (int)(i / Nx), ii = (int)(i - (int64_t)j * Nx);
+    double x = init ? (double)ii : px[i];
+    double y = init ? (double)j : py[i];
+    for (int n = n_lo; n < n_hi; ++n) {
+        const double* P = phi + (int64_t)(n - g.t0) * g.nxy;
+        const int tx = trunc_clamp(x, Nx - 2), ty = trunc_clamp(y, Ny - 2);
+        const double dX = x - tx, dY = y - ty;
+        const double w1 = (1 - dY) * (1 - dX), w2 = dX * (1 - dY), w3 = dY * dX, w4 = (1 - dX) * dY;
+        const double u00 = un_at(P, Nx, ty, tx), u01 = un_at(P, Nx, ty, tx + 1);
+        const double u11 = un_at(P, Nx, ty + 1, tx + 1), u10 = un_at(P, Nx, ty + 1, tx);
+        const double v00 = vn_at(P, Nx, Ny, ty, tx), v01 = vn_at(P, Nx, Ny, ty, tx + 1);
+        const double v11 = vn_at(P, Nx, Ny, ty + 1, tx + 1), v10 = vn_at(P, Nx, Ny, ty + 1, tx);
+        x += w1 * u00 + w2 * u01 + w3 * u11 + w4 * u10;
+        y += w1 * v00 + w2 * v01 + w3 * v11 + w4 * v10;
+    }
+    px[i] = x;
+    py[i] = y;
+}
+
+hipError_t launch_traj(const Geo& g, const double* phi, int n_lo, int n_hi, double* px, double* py, int init,
+                       hipStream_t s) {
+    k_traj<<<flat_blocks(g.nxy), NT, 0, s>>>(g, phi, n_lo, n_hi, px, py, init);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(NT) void k_flow_uv(int Nx, int Ny, const double* __restrict__ px,
+                                                const double* __restrict__ py, double* __restrict__ u,
+                                                double* __restrict__ v) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= (int64_t)Nx * Ny) return;
+    const int j = (int)(i / Nx), ii = (int)(i - (int64_t)j * Nx);
+    u[i] = px[i] - (double)ii;
+    v[i] = py[i] - (double)j;
+}
+
+hipError_t launch_flow_finish(int Nx, int Ny, const double* px, const double* py, double* u, double* v, double* m,
+                              hipStream_t s) {
+    k_flow_uv<<<flat_blocks((int64_t)Nx * Ny), NT, 0, s>>>(Nx, Ny, px, py, u, v);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_div2(Nx, Ny, u, v, m, 1, -1.0, s);   // m = -div(bc 'D') [u; v]
+}
+
+}  // namespace foto
+
+namespace foto {
+
+// x.x partial sums -> gath[rank] (used to seed CG with b.b when b comes from the host)
+__global__ __launch_bounds__(NT) void k_dot_self(int64_t n, const double* __restrict__ x, RedBuf rb, double* gath,
+                                                 int rank) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += x[i] * x[i];
+    double v[1] = {acc}, tot[1];
+    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
+}
+
+hipError_t launch_dot_self(int64_t n, const double* x, RedBuf rb, double* gath, int rank, hipStream_t s) {
+    int nb = (int)std::min<int64_t>((n + NT - 1) / NT, 2048);
+    k_dot_self<<<nb, NT, 0, s>>>(n, x, rb, gath, rank);
+    return hipGetLastError();
+}
+
+}  // namespace foto

@@ -1,0 +1,175 @@
+"""Benamou-Brenier (FOTO) solver on the GPU: Python face of libfoto's BB context.
+
+``solve`` keeps the reference signature and stdout of ``benamou_brenier.solve``
+(benamou_brenier.py:151-271): one line ``f"{crit} ({i+1}/{max_it})"`` per outer
+iteration (Python ``str`` of a float64), the CG non-convergence warning of
+benamou_brenier.py:86-87, and (u, v, m) from the trajectory flow extraction.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr, f64, lib
+
+CG_STENCIL = 0
+CG_SPECTRAL = 1
+
+
+class BBSolver:
+    """Device-resident Benamou-Brenier state (mu, q, phi stay in HBM between calls).
+
+    Parameters mirror ``benamou_brenier.solve``; ``cg_mode`` picks the Poisson CG
+    (0 = 7-point stencil CG, 1 = the same CG run in the DCT-II eigenbasis of A);
+    ``rank/world/nccl_id`` shard the time axis over processes (RCCL),
+    ``virtual_ranks`` shards it in-process on one device (test path).
+    """
+
+    def __init__(self, rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-3, *, device=-1, cg_rtol=1e-6,
+                 cg_maxiter=1000, cg_mode=CG_STENCIL, rank=0, world=1, nccl_id=None, virtual_ranks=1,
+                 timing=False):
+        Nt, Nx, Ny = int(Nt), int(Nx), int(Ny)
+        if Nt < 2:
+            raise ZeroDivisionError("Nt must be >= 2 (benamou_brenier.py:194 divides by Nt - 1)")
+        self.Nt, self.Nx, self.Ny = Nt, Nx, Ny
+        self.r = float(r)
+        self.eps = float(reg_epsilon)
+        nxy = Nx * Ny
+        self._rho0 = f64(rho0, nxy, "rho0")
+        self._rhoT = f64(rhoT, nxy, "rhoT")
+        o = _lib.BBOpts()
+        lib().foto_bb_opts_default(ctypes.byref(o))
+        o.device = int(device)
+        o.cg_rtol = float(cg_rtol)
+        o.cg_maxiter = int(cg_maxiter)
+        o.cg_mode = int(cg_mode)
+        o.rank = int(rank)
+        o.world = int(world)
+        self._id = None
+        if nccl_id is not None:
+            self._id = ctypes.create_string_buffer(bytes(nccl_id), 128)
+            o.nccl_id = ctypes.cast(self._id, ctypes.c_void_p)
+        o.virtual_ranks = int(virtual_ranks)
+        o.timing = 1 if timing else 0
+        self._ctx = ctypes.c_void_p()
+        check(lib().foto_bb_create(dptr(self._rho0), dptr(self._rhoT), Nt, Nx, Ny, self.r, self.eps,
+                                   ctypes.byref(o), ctypes.byref(self._ctx)))
+        self.world = int(world)
+        self.rank = int(rank)
+        self.crit = []
+        self.cg_its = []
+        self.cg_info = []
+
+    # -------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            lib().foto_bb_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -------------------------------------------------------------- iterations
+    def iterate(self, n, convergence_tol=0.0, stop_rules=True, callback=None):
+        """Run up to n outer iterations; returns True if a reference stop rule fired.
+        ``callback(i, crit, cg_its, cg_info)`` is called after each iteration."""
+        errors = []
+
+        def _cb(user, it, crit, its, info):
+            try:
+                self.crit.append(crit)
+                self.cg_its.append(its)
+                self.cg_info.append(info)
+                if callback is not None:
+                    callback(it, crit, its, info)
+            except BaseException as e:   # never let an exception unwind through C
+                errors.append(e)
+
+        cb = _lib.ITER_CB(_cb)
+        done = ctypes.c_int(0)
+        rc = lib().foto_bb_iterate(self._ctx, int(n), float(convergence_tol), 1 if stop_rules else 0, cb, None,
+                                   ctypes.byref(done))
+        if errors:
+            raise errors[0]
+        check(rc)
+        return rc == 1
+
+    def flow(self):
+        """(u, v, m) from the last phi (rank 0 gets the arrays; other ranks get None)."""
+        nxy = self.Nx * self.Ny
+        if self.world > 1 and self.rank != 0:
+            check(lib().foto_bb_flow(self._ctx, None, None, None))
+            return None
+        u = np.empty(nxy)
+        v = np.empty(nxy)
+        m = np.empty(nxy)
+        check(lib().foto_bb_flow(self._ctx, dptr(u), dptr(v), dptr(m)))
+        return u, v, m
+
+    def shard(self):
+        t0 = ctypes.c_int()
+        nl = ctypes.c_int()
+        check(lib().foto_bb_shard(self._ctx, ctypes.byref(t0), ctypes.byref(nl)))
+        return t0.value, nl.value
+
+    def phi(self):
+        _, nl = self.shard()
+        out = np.empty(nl * self.Nx * self.Ny)
+        check(lib().foto_bb_get_phi(self._ctx, dptr(out)))
+        return out
+
+    def state(self):
+        _, nl = self.shard()
+        n = nl * self.Nx * self.Ny
+        mu = np.empty(3 * n)
+        q = np.empty(3 * n)
+        check(lib().foto_bb_get_state(self._ctx, dptr(mu), dptr(q)))
+        return mu, q
+
+    def stats(self):
+        st = _lib.BBStats()
+        check(lib().foto_bb_stats_get(self._ctx, ctypes.byref(st)))
+        d = {f: getattr(st, f) for f in ("outer_iters", "cg_iters_total", "last_crit", "ms_rhs", "ms_cg",
+                                         "ms_prox", "ms_flow")}
+        d["kernels"] = {name: {"n": int(st.n_k[i]), "ms": float(st.ms_k[i]), "bytes": float(st.bytes_k[i])}
+                        for i, name in enumerate(_lib.K_NAMES) if st.n_k[i] > 0}
+        return d
+
+    def reset_stats(self):
+        check(lib().foto_bb_stats_reset(self._ctx))
+
+    def set_timing(self, on):
+        check(lib().foto_bb_set_timing(self._ctx, 1 if on else 0))
+
+    def sync(self):
+        check(lib().foto_bb_sync(self._ctx))
+
+
+def solve(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, max_it=100, *, log=print,
+          stats=None, **opts):
+    """benamou_brenier.solve on the GPU.  Returns (u, v, m)."""
+    if max_it <= 0:
+        # reference: the loop body never runs and `phi` is unbound at benamou_brenier.py:271
+        raise UnboundLocalError("cannot access local variable 'phi' where it is not associated with a value")
+
+    def cb(it, crit, its, info):
+        if info > 0:
+            log(f"WARNING: CG did not converge in {info} iterations.")
+        log(str(np.float64(crit)) + " (" + str(it + 1) + "/" + str(max_it) + ")")
+
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=reg_epsilon, **opts) as s:
+        s.iterate(max_it, convergence_tol=convergence_tol, stop_rules=True, callback=cb)
+        out = s.flow()
+        if stats is not None:
+            stats.update(crit=np.array(s.crit), cg_its=np.array(s.cg_its), cg_info=np.array(s.cg_info),
+                         phi=s.phi(), **s.stats())
+    return out

@@ -1,0 +1,259 @@
+"""HIP path (libfoto.so on the MI355X) against the reference's golden vectors and the oracle.
+
+Tolerances (float64 everywhere):
+  * operators, stepB, RHS, flow extraction: per-voxel arithmetic is in the reference's
+    operation order with no FMA contraction, so these are expected bit-exact; the bar is
+    1e-13 abs (1e-13 rel for the huge-phi flow cases).
+  * CG: same recurrence as scipy; only the dot-product summation order differs, which CG
+    amplifies to ~1e-9 relative in x (kappa ~ 12/eps).  Bar: equal iteration count
+    (+-1 when ||r|| lands within rounding of atol) and 1e-8 * max|x|.
+  * full solve: same outer-iteration count, crit within 1e-7 relative, flow within 1e-7 px.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+foto = pytest.importorskip("foto")
+from foto import ops, gn  # noqa: E402
+from foto.bb import BBSolver, solve  # noqa: E402
+from oracle import foto_oracle as O  # noqa: E402
+
+
+def _grids(d):
+    k = 0
+    while f"g{k}_shape" in d:
+        yield k, tuple(int(s) for s in d[f"g{k}_shape"])
+        k += 1
+
+
+def test_space_time_operators(gold):
+    d = gold("ops.npz")
+    for k, (Nt, Ny, Nx) in _grids(d):
+        phi, w = d[f"g{k}_phi"], d[f"g{k}_w"]
+        np.testing.assert_allclose(ops.grad_st(phi, Nt, Nx, Ny), d[f"g{k}_grad_st"], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(ops.div_st(w, Nt, Nx, Ny), d[f"g{k}_div_st"], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(ops.laplacian_st(phi, Nt, Nx, Ny), d[f"g{k}_lap_st"], rtol=0, atol=1e-13)
+        for r, eps in [(1.0, 1e-2), (1.7, 1e-3)]:
+            np.testing.assert_allclose(ops.apply_A(phi, Nt, Nx, Ny, r, eps), d[f"g{k}_A_{r}_{eps}"], rtol=0,
+                                       atol=1e-13)
+
+
+def test_2d_operators(gold):
+    d = gold("ops.npz")
+    for k, (Nt, Ny, Nx) in _grids(d):
+        f = d[f"g{k}_phi"][: Nx * Ny]
+        uv = d[f"g{k}_w"][: 2 * Nx * Ny]
+        np.testing.assert_allclose(ops.grad2(f, Nx, Ny, "N"), d[f"g{k}_grad2_N"], rtol=0, atol=1e-14)
+        np.testing.assert_allclose(ops.grad2(f, Nx, Ny, "D"), d[f"g{k}_grad2_D"], rtol=0, atol=1e-14)
+        np.testing.assert_allclose(ops.div2(uv, Nx, Ny, "D"), d[f"g{k}_div2_D"], rtol=0, atol=1e-14)
+        np.testing.assert_allclose(ops.div2(uv, Nx, Ny, "N"), d[f"g{k}_div2_N"], rtol=0, atol=1e-14)
+        np.testing.assert_allclose(ops.grad2_forward(f, Nx, Ny), d[f"g{k}_gradf_N"], rtol=0, atol=1e-14)
+    with pytest.raises(NotImplementedError):
+        ops.grad2(np.zeros(12), 4, 3, "X")
+
+
+def test_stepb(gold):
+    d = gold("stepb.npz")
+    M = int(d["M"])
+    np.testing.assert_allclose(ops.stepB(d["p"], M), d["q"], rtol=0, atol=1e-12)
+
+
+def test_stepb_large_properties():
+    rng = np.random.default_rng(7)
+    M = 640 * 480 * 4
+    p = 3.0 * rng.standard_normal(3 * M)
+    q = ops.stepB(p, M)
+    a, b1, b2 = q[:M], q[M:2 * M], q[2 * M:]
+    assert np.all(a + 0.5 * (b1 * b1 + b2 * b2) <= 1e-11)
+    sel = rng.choice(M, 20000, replace=False)
+    ps = np.concatenate([p[sel], p[M + sel], p[2 * M + sel]])
+    np.testing.assert_allclose(np.concatenate([a[sel], b1[sel], b2[sel]]), O.stepB(ps, sel.size), rtol=0, atol=1e-12)
+
+
+def test_bb_rhs(gold):
+    d = gold("bbstep.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, eps = d["r_eps"]
+    F = ops.bb_rhs(d["mu"], d["q"], d["rho0"], d["rhoT"], r, Nt, Nx, Ny)
+    np.testing.assert_allclose(F, d["F"], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("mode", [0])
+def test_cg(gold, mode):
+    d = gold("cg.npz")
+    for c in range(3):
+        Nt, Ny, Nx = (int(s) for s in d[f"c{c}_shape"])
+        r, eps = d[f"c{c}_r_eps"]
+        x, info, its = ops.cg(d[f"c{c}_b"], Nt, Nx, Ny, r, eps, 1e-6, 1000, mode)
+        assert info == 0
+        assert abs(its - int(d[f"c{c}_its"])) <= 1
+        ref = d[f"c{c}_x"]
+        np.testing.assert_allclose(x, ref, rtol=0, atol=1e-8 * np.abs(ref).max())
+        x5, info5, its5 = ops.cg(d[f"c{c}_b"], Nt, Nx, Ny, r, eps, 1e-6, 5, mode)
+        assert info5 == 5 and its5 == 5
+        np.testing.assert_allclose(x5, d[f"c{c}_x_max5"], rtol=0, atol=1e-10 * np.abs(d[f"c{c}_x_max5"]).max())
+
+
+def test_cg_zero_rhs():
+    x, info, its = ops.cg(np.zeros(4 * 5 * 6), 4, 6, 5, 1.0, 1e-2)
+    assert info == 0 and its == 0 and not np.any(x)
+
+
+def test_bb_step_cg(gold):
+    d = gold("bbstep.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, eps = d["r_eps"]
+    F = ops.bb_rhs(d["mu"], d["q"], d["rho0"], d["rhoT"], r, Nt, Nx, Ny)
+    phi, info, its = ops.cg(F, Nt, Nx, Ny, r, eps)
+    np.testing.assert_allclose(phi, d["phi"], rtol=0, atol=1e-8 * np.abs(d["phi"]).max())
+
+
+def test_flow(gold):
+    d = gold("flow.npz")
+    for f in range(4):
+        Nt, Ny, Nx = (int(s) for s in d[f"f{f}_shape"])
+        u, v, m = ops.flow_from_phi(d[f"f{f}_phi"], Nt, Nx, Ny)
+        np.testing.assert_allclose(u, d[f"f{f}_u"], rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(v, d[f"f{f}_v"], rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(m, d[f"f{f}_m"], rtol=1e-13, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["bb_small.npz", "bb_tex.npz"])
+def test_bb_solve_small(gold, name, capsys):
+    d = gold(name)
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    st = {}
+    u, v, m = solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=int(max_it),
+                    stats=st)
+    assert len(st["crit"]) == len(d["crit"])
+    assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
+    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-7, atol=0)
+    np.testing.assert_allclose(st["phi"], d["phi"], rtol=0, atol=1e-7 * np.abs(d["phi"]).max())
+    for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
+    out = capsys.readouterr().out.splitlines()
+    assert len(out) == len(d["crit"])
+    assert out[-1].endswith(f"({len(d['crit'])}/{int(max_it)})")
+
+
+def test_bb_solve_c1(gold):
+    d = gold("bb_c1.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    st = {}
+    u, v, m = solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=int(max_it),
+                    stats=st, log=lambda s: None)
+    assert len(st["crit"]) == len(d["crit"]) == 46
+    assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
+    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-6, atol=0)
+    for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("vr", [2, 3])
+def test_bb_virtual_ranks_match_single(gold, vr):
+    """The time-sharded path (halo planes, per-rank partial sums, trajectory relay) on one
+    device with `vr` in-process shards reproduces the single-shard solve."""
+    d = gold("bb_tex.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    res = []
+    for v_ in (1, vr):
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, virtual_ranks=v_) as s:
+            s.iterate(int(max_it), tol, True)
+            res.append((np.array(s.crit), np.array(s.cg_its), s.phi(), s.flow()))
+    (c1, k1, p1, f1), (c2, k2, p2, f2) = res
+    assert len(c1) == len(c2)
+    assert np.max(np.abs(k1 - k2)) <= 1
+    np.testing.assert_allclose(c2, c1, rtol=1e-9)
+    np.testing.assert_allclose(p2, p1, rtol=0, atol=1e-8 * np.abs(p1).max())
+    for a, b in zip(f1, f2):
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-8)
+
+
+def test_bb_solver_state_and_stats(gold):
+    d = gold("bb_small.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, _ = d["params"]
+    with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, timing=True) as s:
+        stopped = s.iterate(3, 0.0, False)
+        assert not stopped and len(s.crit) == 3
+        np.testing.assert_allclose(s.crit, d["crit"][:3], rtol=1e-7)
+        mu, q = s.state()
+        N = Nt * Nx * Ny
+        assert mu.shape == (3 * N,) and np.all(mu[:N] >= 0)
+        st = s.stats()
+        assert st["outer_iters"] == 3
+        assert st["kernels"]["cg_dir"]["n"] == st["cg_iters_total"]
+        assert st["kernels"]["cg_upd"]["n"] == st["cg_iters_total"]
+
+
+def test_bb_errors():
+    z = np.zeros(12)
+    with pytest.raises(ZeroDivisionError):
+        BBSolver(z, z, 1, 4, 3)
+    with pytest.raises(UnboundLocalError):
+        solve(z, z, 4, 4, 3, max_it=0)
+    with pytest.raises(foto.FotoError):
+        BBSolver(z[:2], z[:2], 4, 2, 1)
+
+
+# ---------------------------------------------------------------- full-size properties (bench grid)
+
+def test_full_size_operator_properties():
+    Nt, Ny, Nx = 32, 480, 640
+    N = Nt * Ny * Nx
+    r, eps = 1.0, 1e-2
+    one = np.ones(N)
+    np.testing.assert_array_equal(ops.apply_A(one, Nt, Nx, Ny, r, eps), np.full(N, r * eps))
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(N)
+    y = rng.standard_normal(N)
+    Ax, Ay = ops.apply_A(x, Nt, Nx, Ny, r, eps), ops.apply_A(y, Nt, Nx, Ny, r, eps)
+    assert abs(x @ Ay - y @ Ax) <= 1e-10 * abs(x @ Ay)     # symmetry
+    assert x @ Ax > 0                                       # positive definite direction
+    # L_st annihilates constants and linear functions in the interior
+    lin = np.tile(np.arange(Nx, dtype=np.float64), Nt * Ny)
+    Ll = ops.laplacian_st(lin, Nt, Nx, Ny).reshape(Nt, Ny, Nx)
+    assert np.all(Ll[:, :, 1:-1] == 0)
+
+
+def test_full_size_cg_true_residual():
+    from foto.synthetic import translating_gaussian
+    Nt, Ny, Nx = 32, 480, 640
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2) as s:
+        s.iterate(1, 0.0, False)
+        phi = s.phi()
+        assert 100 < s.cg_its[0] < 1000
+    N = Nt * Nx * Ny
+    mu0 = np.concatenate([np.concatenate([(1 - n / (Nt - 1)) * rho0 + (n / (Nt - 1)) * rhoT for n in range(Nt)]),
+                          np.zeros(2 * N)])
+    F = ops.bb_rhs(mu0, np.zeros(3 * N), rho0, rhoT, 1.0, Nt, Nx, Ny)
+    res = F - ops.apply_A(phi, Nt, Nx, Ny, 1.0, 1e-2)
+    assert np.linalg.norm(res) <= 1.01e-6 * np.linalg.norm(F)
+
+
+# ---------------------------------------------------------------- GN
+
+def test_gn_operator(gold):
+    d = gold("gn.npz")
+    for g in range(2):
+        w, h = (int(s) for s in d[f"n{g}_wh"])
+        alpha, lam = d[f"n{g}_alpha_lambda"]
+        f1, f2 = d[f"n{g}_f1"], d[f"n{g}_f2"]
+        np.testing.assert_allclose(gn.apply(f1, f2, w, h, alpha, lam, d[f"n{g}_x"]), d[f"n{g}_Ax"], rtol=0, atol=1e-13)
+        np.testing.assert_array_equal(gn.rhs(f1, f2, w, h), d[f"n{g}_b"])
+
+
+def test_gn_solve(gold):
+    d = gold("gn.npz")
+    for g in range(2):
+        w, h = (int(s) for s in d[f"n{g}_wh"])
+        alpha, lam = d[f"n{g}_alpha_lambda"]
+        u, v, m, info, its = gn.solve(d[f"n{g}_f1"], d[f"n{g}_f2"], w, h, alpha, lam)
+        assert info == 0 and its > 0
+        for a, b in ((u, d[f"n{g}_u"]), (v, d[f"n{g}_v"]), (m, d[f"n{g}_m"])):
+            np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
