@@ -186,8 +186,10 @@ def test_bb_solver_state_and_stats(gold):
         assert mu.shape == (3 * N,) and np.all(mu[:N] >= 0)
         st = s.stats()
         assert st["outer_iters"] == 3
-        assert st["kernels"]["cg_dir"]["n"] == st["cg_iters_total"]
-        assert st["kernels"]["cg_upd"]["n"] == st["cg_iters_total"]
+        # launches include the early-exit ones queued past convergence (host polls in chunks)
+        assert st["kernels"]["cg_dir"]["n"] >= st["cg_iters_total"]
+        assert st["kernels"]["cg_upd"]["n"] >= st["cg_iters_total"]
+        assert st["kernels"]["cg_dir"]["n"] <= st["cg_iters_total"] + 3 * 8
 
 
 def test_bb_errors():
