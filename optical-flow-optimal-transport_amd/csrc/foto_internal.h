@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -66,6 +67,62 @@ struct RedBuf {
     unsigned* ticket;
     int cap;   // blocks * quantities capacity
 };
+
+// ----------------------------------------------------------------------------- per-launch timing
+
+struct KTimer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    struct Pend { hipEvent_t a, b; int cls; double bytes; };
+    std::vector<Pend> pend;
+    int64_t n[8] = {0};
+    double ms[8] = {0};
+    double bytes[8] = {0};
+
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    // returns the start event to be paired by stop()
+    hipEvent_t start(hipStream_t s) {
+        if (!on) return nullptr;
+        hipEvent_t e = get();
+        if (e) (void)hipEventRecord(e, s);
+        return e;
+    }
+    void stop(hipEvent_t a, hipStream_t s, int cls, double by) {
+        if (!on || !a) return;
+        hipEvent_t b = get();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        pend.push_back({a, b, cls, by});
+    }
+    void resolve() {   // call after a stream sync
+        for (auto& p : pend) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+                n[p.cls] += 1;
+                ms[p.cls] += t;
+                bytes[p.cls] += p.bytes;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pend.clear();
+    }
+    void reset() {
+        std::fill(n, n + 8, 0);
+        std::fill(ms, ms + 8, 0.0);
+        std::fill(bytes, bytes + 8, 0.0);
+    }
+    ~KTimer() {
+        for (auto& p : pend) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
 
 // ----------------------------------------------------------------------------- kernel launchers
 // (defined in foto_kernels.hip; all enqueue on `s` and never synchronise)

@@ -1,0 +1,505 @@
+// Spectral CG for the stepA Poisson solve (benamou_brenier.py:85) -- gfx950.
+//
+// A = -r L_st + r eps I with the Neumann lap1d stencils of operators.py:95-110 is
+// diagonalised exactly by the orthonormal DCT-II along each axis:
+//     A = C^T diag(lam) C,  C = Ct (x) Cy (x) Cx,
+//     lam(kt,ky,kx) = r eps + r (mu_t[kt] + mu_y[ky] + mu_x[kx]),  mu_n[k] = 2 - 2 cos(pi k / n).
+// CG is basis-invariant: running scipy's CG recurrence on (diag(lam), C b) produces C x_k
+// for the same x_k, the same residual norms, hence the same stopping iteration (up to
+// rounding).  In that basis every CG iteration is pointwise, so one pass per iteration
+// (Chronopoulos-Gear form: p.Ap from r.Ar, one fused reduction) reads and writes only r
+// and p; x is recovered at the end as x = C^T ((b^ - r^) / lam).  The two vectors
+// (2 x 78.6 MB at 640x480x32) stay resident in the 256 MiB Infinity Cache.
+//
+// The per-axis DCTs are GEMMs (n x n matrix applied along an axis) on f64 MFMA
+// (v_mfma_f64_16x16x4_f64), 64x64x16 block tiles staged through LDS.
+#include <cmath>
+#include <memory>
+
+#include "foto_spectral.h"
+
+namespace foto {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+// ============================================================================ reductions (local copies)
+
+__device__ __forceinline__ double sp_wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;
+}
+
+template <int K>
+__device__ __forceinline__ void sp_block_sum(double (&v)[K], double* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        v[k] = sp_wave_sum(v[k]);
+        if (lane == 0) sh[k * (NT / 64) + w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double s = sh[k * (NT / 64)];
+#pragma unroll
+            for (int j = 1; j < NT / 64; ++j) s += sh[k * (NT / 64) + j];
+            v[k] = s;
+        }
+    }
+}
+
+template <int K>
+__device__ bool sp_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
+    __shared__ double sh[K * (NT / 64)];
+    __shared__ int is_last;
+    sp_block_sum<K>(v, sh);
+    const int nb = gridDim.x;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            __hip_atomic_store(&rb.partials[(int64_t)k * nb + blockIdx.x], v[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(rb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (t == (unsigned)(nb - 1));
+    }
+    __syncthreads();
+    if (!is_last) return false;
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < nb; i += NT) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            acc[k] += __hip_atomic_load(&rb.partials[(int64_t)k * nb + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sp_block_sum<K>(acc, sh);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) tot[k] = acc[k];
+        __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
+// ============================================================================ DCT along one axis (f64 MFMA GEMM)
+
+constexpr int BM = 64, BN = 64, BK = 16;
+constexpr int AS_LD = BK + 1;   // 17 doubles: column reads across 16 rows hit 16 distinct bank pairs
+constexpr int BS_LD = BN + 16;  // 80 doubles = 160 dwords = 32 mod 64: the 4 k-rows of a read split the banks
+
+// out[o][k][i] = sum_j M[k][j] in[o][j][i] over an array viewed as [outer][n][inner].
+// CONTIG (inner == 1): GEMM rows = o, cols = k   (A = in rows, B = M^T)
+// otherwise          : GEMM rows = k, cols = i, batch o = blockIdx.z (A = M, B = in[o])
+template <bool CONTIG>
+__global__ __launch_bounds__(256) void k_dct_axis(int outer, int n, int inner, const double* __restrict__ M,
+                                                  const double* __restrict__ in, double* __restrict__ out) {
+    __shared__ double As[BM * AS_LD];
+    __shared__ double Bs[BK * BS_LD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    int row0, col0;
+    const double* inb;
+    double* outb;
+    int nrows, ncols;
+    if (CONTIG) {
+        row0 = blockIdx.y * BM;   // o
+        col0 = blockIdx.x * BN;   // k
+        nrows = outer;
+        ncols = n;
+        inb = in;
+        outb = out;
+    } else {
+        row0 = blockIdx.y * BM;   // k
+        col0 = blockIdx.x * BN;   // i
+        nrows = n;
+        ncols = inner;
+        inb = in + (int64_t)blockIdx.z * n * inner;
+        outb = out + (int64_t)blockIdx.z * n * inner;
+    }
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+    for (int j0 = 0; j0 < n; j0 += BK) {
+        // ---- stage A (BM x BK) and B (BK x BN)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            {   // A[m][kk]
+                const int m = e >> 4, kk = e & 15;
+                const int gr = row0 + m, gj = j0 + kk;
+                double v = 0.0;
+                if (gr < nrows && gj < n) v = CONTIG ? inb[(int64_t)gr * n + gj] : M[(int64_t)gr * n + gj];
+                As[m * AS_LD + kk] = v;
+            }
+            if (CONTIG) {   // B[kk][c] = M[col0 + c][j0 + kk]
+                const int c = e >> 4, kk = e & 15;
+                const int gk = col0 + c, gj = j0 + kk;
+                Bs[kk * BS_LD + c] = (gk < ncols && gj < n) ? M[(int64_t)gk * n + gj] : 0.0;
+            } else {        // B[kk][c] = in[j0 + kk][col0 + c]
+                const int kk = e >> 6, c = e & 63;
+                const int gj = j0 + kk, gi = col0 + c;
+                Bs[kk * BS_LD + c] = (gj < n && gi < ncols) ? inb[(int64_t)gj * inner + gi] : 0.0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k4 = 0; k4 < BK / 4; ++k4) {
+            const int kk = k4 * 4 + (lane >> 4);
+            double a[2], b[2];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) a[mi] = As[(wm * 32 + mi * 16 + (lane & 15)) * AS_LD + kk];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b[ni] = Bs[kk * BS_LD + wn * 32 + ni * 16 + (lane & 15)];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // ---- store: D[row = (lane>>4) + 4 r][col = lane & 15]
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gr = row0 + wm * 32 + mi * 16 + (lane >> 4) + 4 * r;
+                const int gc = col0 + wn * 32 + ni * 16 + (lane & 15);
+                if (gr < nrows && gc < ncols) {
+                    if (CONTIG) outb[(int64_t)gr * n + gc] = acc[mi][ni][r];
+                    else outb[(int64_t)gr * inner + gc] = acc[mi][ni][r];
+                }
+            }
+}
+
+static hipError_t dct_axis(int outer, int n, int inner, const double* M, const double* in, double* out,
+                           hipStream_t s) {
+    if (inner == 1) {
+        dim3 grid((n + BN - 1) / BN, (outer + BM - 1) / BM, 1);
+        k_dct_axis<true><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+    } else {
+        dim3 grid((inner + BN - 1) / BN, (n + BM - 1) / BM, outer);
+        k_dct_axis<false><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+    }
+    return hipGetLastError();
+}
+
+// ============================================================================ CG in the eigenbasis
+
+struct SpecTab {
+    const double* mt;   // mu_t[kt]
+    const double* my;   // mu_y[ky]
+    const double* mx;   // mu_x[kx]
+    double r, reps;     // r, r * eps
+    int Nt, Ny, Nx;
+};
+
+__device__ __forceinline__ double spec_lam(const SpecTab& T, double rowmu, int kx) {
+    return T.reps + T.r * (rowmu + T.mx[kx]);
+}
+
+// tile = 4 rows x 128 columns; thread (tx, ty) owns columns 2tx, 2tx+1 of row ty.
+// f(i, lam0, lam1, n2): elements i and i+1 (n2 = number valid: 1 or 2).  With Nx even,
+// i is even and both elements are 16-B aligned (one dwordx4 per lane).
+template <class F>
+__device__ __forceinline__ void spec_for_each(const SpecTab& T, F f) {
+    const int rows = T.Nt * T.Ny;
+    const int ntx = (T.Nx + 127) / 128;
+    const int ntiles = ntx * ((rows + 3) / 4);
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int row = (t / ntx) * 4 + ty;
+        const int kx = (t % ntx) * 128 + 2 * tx;
+        if (row >= rows || kx >= T.Nx) continue;
+        const int kt = row / T.Ny, ky = row - kt * T.Ny;
+        const double rowmu = T.mt[kt] + T.my[ky];
+        const int64_t i = (int64_t)row * T.Nx + kx;
+        const int n2 = (kx + 1 < T.Nx) ? 2 : 1;
+        f(i, spec_lam(T, rowmu, kx), n2 == 2 ? spec_lam(T, rowmu, kx + 1) : 1.0, n2);
+    }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void ld2(const double* p, int64_t i, int n2, double& a, double& b) {
+    if (VEC && n2 == 2) {
+        const dbl2 v = *reinterpret_cast<const dbl2*>(p + i);
+        a = v[0];
+        b = v[1];
+    } else {
+        a = p[i];
+        b = (n2 == 2) ? p[i + 1] : 0.0;
+    }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void st2(double* p, int64_t i, int n2, double a, double b) {
+    if (VEC && n2 == 2) {
+        *reinterpret_cast<dbl2*>(p + i) = dbl2{a, b};
+    } else {
+        p[i] = a;
+        if (n2 == 2) p[i + 1] = b;
+    }
+}
+
+// r^ = b^; partials (r.r, r.lam.r) -> gath[0..1]
+template <bool VEC>
+__global__ __launch_bounds__(NT) void k_spec_init(SpecTab T, const double* __restrict__ bh, double* __restrict__ rh,
+                                                  RedBuf rb, double* gath) {
+    double a0 = 0.0, a1 = 0.0;
+    spec_for_each(T, [&](int64_t i, double l0, double l1, int n2) {
+        double b0, b1;
+        ld2<VEC>(bh, i, n2, b0, b1);
+        st2<VEC>(rh, i, n2, b0, b1);
+        a0 += b0 * b0;
+        a1 += l0 * (b0 * b0);
+        if (n2 == 2) {
+            a0 += b1 * b1;
+            a1 += l1 * (b1 * b1);
+        }
+    });
+    double v[2] = {a0, a1}, tot[2];
+    if (sp_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) { gath[0] = tot[0]; gath[1] = tot[1]; }
+}
+
+// One CG iteration k (Chronopoulos-Gear): given rho_k = r.r and m_k = r.lam.r (gathered),
+//   stop if ||r_k|| < atol (scipy's top-of-loop test); beta = rho_k / rho_{k-1};
+//   p.Ap = m_k - beta rho_k / alpha_{k-1} (k > 0), = m_0 (k = 0); alpha = rho_k / p.Ap;
+//   p = beta p + r;  r = r - alpha (lam p);  partials (r.r, r.lam.r) of r_{k+1}.
+template <bool VEC>
+__global__ __launch_bounds__(NT) void k_spec_cg(SpecTab T, int k, double* __restrict__ rh, double* __restrict__ ph,
+                                                CGScal* S, RedBuf rb, double* gath, double rtol) {
+    if (S->done) return;
+    const double rho = gath[0], mk = gath[1];
+    double atol, beta = 0.0, pap;
+    if (k == 0) {
+        atol = fmax(0.0, rtol * sqrt(rho));
+        if (rho == 0.0) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) { S->done = 1; S->iters = 0; }
+            return;
+        }
+        pap = mk;
+    } else {
+        atol = S->atol;
+        beta = rho / S->rho;
+        pap = mk - beta * rho / S->pap;   // S->pap holds alpha_{k-1}
+    }
+    if (sqrt(rho) < atol) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { S->done = 1; S->iters = k; }
+        return;
+    }
+    const double alpha = rho / pap;
+    double a0 = 0.0, a1 = 0.0;
+    spec_for_each(T, [&](int64_t i, double l0, double l1, int n2) {
+        double r0, r1, p0 = 0.0, p1 = 0.0;
+        ld2<VEC>(rh, i, n2, r0, r1);
+        if (k > 0) ld2<VEC>(ph, i, n2, p0, p1);
+        p0 = (k == 0) ? r0 : beta * p0 + r0;
+        p1 = (k == 0) ? r1 : beta * p1 + r1;
+        const double n0 = r0 - alpha * (l0 * p0);
+        const double n1 = r1 - alpha * (l1 * p1);
+        st2<VEC>(ph, i, n2, p0, p1);
+        st2<VEC>(rh, i, n2, n0, n1);
+        a0 += n0 * n0;
+        a1 += l0 * (n0 * n0);
+        if (n2 == 2) {
+            a0 += n1 * n1;
+            a1 += l1 * (n1 * n1);
+        }
+    });
+    double v[2] = {a0, a1}, tot[2];
+    if (sp_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) {
+        S->rho = rho;
+        S->pap = alpha;
+        if (k == 0) { S->atol = atol; S->bb = rho; }
+        gath[0] = tot[0];
+        gath[1] = tot[1];
+    }
+}
+
+// x^ = (b^ - r^) / lam
+template <bool VEC>
+__global__ __launch_bounds__(NT) void k_spec_xhat(SpecTab T, const double* __restrict__ bh,
+                                                  const double* __restrict__ rh, double* __restrict__ xh) {
+    spec_for_each(T, [&](int64_t i, double l0, double l1, int n2) {
+        double b0, b1, r0, r1;
+        ld2<VEC>(bh, i, n2, b0, b1);
+        ld2<VEC>(rh, i, n2, r0, r1);
+        st2<VEC>(xh, i, n2, (b0 - r0) / l0, (b1 - r1) / l1);
+    });
+}
+
+// ============================================================================ plan
+
+struct SpecImpl {
+    Geo g{};
+    double r = 1, eps = 0;
+    double *bh = nullptr, *rh = nullptr, *ph = nullptr, *tmp = nullptr;
+    double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
+    double *mx = nullptr, *my = nullptr, *mt = nullptr;
+    RedBuf rb{};
+    double* gath = nullptr;
+    CGScal* S = nullptr;
+    CGScal* hS = nullptr;
+    std::vector<void*> allocs;
+    int nblocks = 0;
+
+    int alloc(size_t bytes, void** p) {
+        FOTO_HIP_CHECK(hipMalloc(p, bytes));
+        allocs.push_back(*p);
+        return 0;
+    }
+    ~SpecImpl() {
+        for (void* p : allocs) (void)hipFree(p);
+        if (hS) (void)hipHostFree(hS);
+    }
+    SpecTab tab() const {
+        SpecTab T;
+        T.mt = mt; T.my = my; T.mx = mx; T.r = r; T.reps = r * eps;
+        T.Nt = g.Nt; T.Ny = g.Ny; T.Nx = g.Nx;
+        return T;
+    }
+};
+
+// orthonormal DCT-II matrix C[k][j] = s_k cos(pi k (2j+1) / (2n)) (long double on the host)
+static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, std::vector<double>& mu) {
+    C.assign((size_t)n * n, 0.0);
+    CT.assign((size_t)n * n, 0.0);
+    mu.assign(n, 0.0);
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int k = 0; k < n; ++k) {
+        const long double s = (k == 0) ? sqrtl(1.0L / n) : sqrtl(2.0L / n);
+        for (int j = 0; j < n; ++j) {
+            const double v = (double)(s * cosl(pi * k * (2.0L * j + 1.0L) / (2.0L * n)));
+            C[(size_t)k * n + j] = v;
+            CT[(size_t)j * n + k] = v;
+        }
+        mu[k] = (double)(2.0L - 2.0L * cosl(pi * k / n));
+    }
+}
+
+int SpectralPlan::init(const Geo& g, int world, double r, double eps, hipStream_t s) {
+    if (world != 1 || g.nloc != g.Nt) {
+        set_error("spectral CG needs the whole time axis on one shard");
+        return FOTO_ERR_ARG;
+    }
+    if (!(eps > 0.0)) {
+        set_error("spectral CG needs reg_epsilon > 0 (x = (b - r) / lam)");
+        return FOTO_ERR_ARG;
+    }
+    auto* P = new SpecImpl();
+    impl = P;
+    P->g = g;
+    P->r = r;
+    P->eps = eps;
+    const size_t N = (size_t)g.Nt * g.nxy;
+    void* b;
+    FOTO_TRY(P->alloc(N * 8, &b)); P->bh = (double*)b;
+    FOTO_TRY(P->alloc(N * 8, &b)); P->rh = (double*)b;
+    FOTO_TRY(P->alloc(N * 8, &b)); P->ph = (double*)b;
+    FOTO_TRY(P->alloc(N * 8, &b)); P->tmp = (double*)b;
+    std::vector<double> C, CT, mu;
+    auto up = [&](int n, double** Cd, double** CTd, double** mud) -> int {
+        dct_matrix(n, C, CT, mu);
+        void* p;
+        FOTO_TRY(P->alloc(C.size() * 8, &p)); *Cd = (double*)p;
+        FOTO_TRY(P->alloc(CT.size() * 8, &p)); *CTd = (double*)p;
+        FOTO_TRY(P->alloc(mu.size() * 8, &p)); *mud = (double*)p;
+        FOTO_HIP_CHECK(hipMemcpy(*Cd, C.data(), C.size() * 8, hipMemcpyHostToDevice));
+        FOTO_HIP_CHECK(hipMemcpy(*CTd, CT.data(), CT.size() * 8, hipMemcpyHostToDevice));
+        FOTO_HIP_CHECK(hipMemcpy(*mud, mu.data(), mu.size() * 8, hipMemcpyHostToDevice));
+        return 0;
+    };
+    FOTO_TRY(up(g.Nx, &P->Cx, &P->CxT, &P->mx));
+    FOTO_TRY(up(g.Ny, &P->Cy, &P->CyT, &P->my));
+    FOTO_TRY(up(g.Nt, &P->Ct, &P->CtT, &P->mt));
+    const int rows = g.Nt * g.Ny;
+    const int ntiles = ((g.Nx + 127) / 128) * ((rows + 3) / 4);
+    P->nblocks = std::min(ntiles, 2048);
+    FOTO_TRY(P->alloc(sizeof(double) * (2 * P->nblocks + 8), &b));
+    P->rb.partials = (double*)b;
+    P->rb.ticket = (unsigned*)((double*)b + 2 * P->nblocks);
+    P->rb.cap = 2 * P->nblocks;
+    FOTO_HIP_CHECK(hipMemset(P->rb.ticket, 0, 8 * sizeof(double)));
+    FOTO_TRY(P->alloc(sizeof(double) * 4, &b)); P->gath = (double*)b;
+    FOTO_TRY(P->alloc(sizeof(CGScal), &b)); P->S = (CGScal*)b;
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
+    (void)s;
+    return 0;
+}
+
+SpectralPlan::~SpectralPlan() { delete (SpecImpl*)impl; }
+
+// 3-D transforms: forward = (Ct (x) Cy (x) Cx), inverse = transpose.
+static int forward3(SpecImpl* P, double* in, double* scratch, double* out, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    // in -x-> scratch -y-> in -t-> out   (in is clobbered)
+    FOTO_HIP_CHECK(dct_axis(g.Nt * g.Ny, g.Nx, 1, P->Cx, in, scratch, s));
+    FOTO_HIP_CHECK(dct_axis(g.Nt, g.Ny, g.Nx, P->Cy, scratch, in, s));
+    FOTO_HIP_CHECK(dct_axis(1, g.Nt, (int)g.nxy, P->Ct, in, out, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    return 0;
+}
+
+static int inverse3(SpecImpl* P, double* in, double* scratch, double* out, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    // in -t-> scratch -y-> in -x-> out   (in is clobbered)
+    FOTO_HIP_CHECK(dct_axis(1, g.Nt, (int)g.nxy, P->CtT, in, scratch, s));
+    FOTO_HIP_CHECK(dct_axis(g.Nt, g.Ny, g.Nx, P->CyT, scratch, in, s));
+    FOTO_HIP_CHECK(dct_axis(g.Nt * g.Ny, g.Nx, 1, P->CxT, in, out, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    return 0;
+}
+
+int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info,
+                        KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    const Geo& g = P->g;
+    const SpecTab T = P->tab();
+    const double N = (double)g.Nt * (double)g.nxy;
+    // b (physical) -> b^ ; b is scratch afterwards
+    const bool vec = (g.Nx % 2) == 0;
+    FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
+    if (vec) k_spec_init<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
+    else k_spec_init<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
+    FOTO_HIP_CHECK(hipGetLastError());
+    FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
+    int k = 0;
+    bool done = false;
+    const int first = predicted > 4 ? predicted - 3 : 8;
+    while (k < maxiter) {
+        int chunk = (k == 0) ? first : 2;
+        chunk = std::min(chunk, maxiter - k);
+        for (int j = 0; j < chunk; ++j, ++k) {
+            hipEvent_t e = kt ? kt->start(s) : nullptr;
+            if (vec) k_spec_cg<true><<<P->nblocks, NT, 0, s>>>(T, k, P->rh, P->ph, P->S, P->rb, P->gath, rtol);
+            else k_spec_cg<false><<<P->nblocks, NT, 0, s>>>(T, k, P->rh, P->ph, P->S, P->rb, P->gath, rtol);
+            FOTO_HIP_CHECK(hipGetLastError());
+            if (kt) kt->stop(e, s, FOTO_K_SPEC, (k == 0 ? 24.0 : 32.0) * N);
+        }
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->hS, P->S, sizeof(CGScal), hipMemcpyDeviceToHost, s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        if (P->hS->done) { done = true; break; }
+    }
+    *iters = done ? P->hS->iters : maxiter;
+    *info = done ? 0 : maxiter;
+    if (vec) k_spec_xhat<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+    else k_spec_xhat<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+    FOTO_HIP_CHECK(hipGetLastError());
+    FOTO_TRY(inverse3(P, P->tmp, b, x, kt, s));
+    return 0;
+}
+
+}  // namespace foto

@@ -79,7 +79,7 @@ def test_bb_rhs(gold):
     np.testing.assert_allclose(F, d["F"], rtol=0, atol=1e-13)
 
 
-@pytest.mark.parametrize("mode", [0])
+@pytest.mark.parametrize("mode", [0, 1])
 def test_cg(gold, mode):
     d = gold("cg.npz")
     for c in range(3):
@@ -119,14 +119,15 @@ def test_flow(gold):
         np.testing.assert_allclose(m, d[f"f{f}_m"], rtol=1e-13, atol=1e-12)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("name", ["bb_small.npz", "bb_tex.npz"])
-def test_bb_solve_small(gold, name, capsys):
+def test_bb_solve_small(gold, name, mode, capsys):
     d = gold(name)
     Nt, Ny, Nx = (int(s) for s in d["shape"])
     r, tol, eps, max_it = d["params"]
     st = {}
     u, v, m = solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=int(max_it),
-                    stats=st)
+                    stats=st, cg_mode=mode)
     assert len(st["crit"]) == len(d["crit"])
     assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
     np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-7, atol=0)
@@ -138,13 +139,14 @@ def test_bb_solve_small(gold, name, capsys):
     assert out[-1].endswith(f"({len(d['crit'])}/{int(max_it)})")
 
 
-def test_bb_solve_c1(gold):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_bb_solve_c1(gold, mode):
     d = gold("bb_c1.npz")
     Nt, Ny, Nx = (int(s) for s in d["shape"])
     r, tol, eps, max_it = d["params"]
     st = {}
     u, v, m = solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=int(max_it),
-                    stats=st, log=lambda s: None)
+                    stats=st, log=lambda s: None, cg_mode=mode)
     assert len(st["crit"]) == len(d["crit"]) == 46
     assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
     np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-6, atol=0)
@@ -209,7 +211,8 @@ def test_full_size_operator_properties():
     N = Nt * Ny * Nx
     r, eps = 1.0, 1e-2
     one = np.ones(N)
-    np.testing.assert_array_equal(ops.apply_A(one, Nt, Nx, Ny, r, eps), np.full(N, r * eps))
+    # A 1 = r eps 1 (L annihilates constants); scipy's CSR row sum rounds the same way (~2e-16)
+    np.testing.assert_allclose(ops.apply_A(one, Nt, Nx, Ny, r, eps), np.full(N, r * eps), rtol=1e-13, atol=0)
     rng = np.random.default_rng(3)
     x = rng.standard_normal(N)
     y = rng.standard_normal(N)
@@ -222,11 +225,28 @@ def test_full_size_operator_properties():
     assert np.all(Ll[:, :, 1:-1] == 0)
 
 
+def test_full_size_spectral_matches_stencil():
+    """Spectral CG (DCT eigenbasis) vs stencil CG on the bench grid: same iteration counts,
+    same phi to CG-rounding level, for two outer iterations."""
+    from foto.synthetic import translating_gaussian
+    Nt, Ny, Nx = 32, 480, 640
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = []
+    for mode in (0, 1):
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
+            s.iterate(2, 0.0, False)
+            out.append((np.array(s.cg_its), np.array(s.crit), s.phi()))
+    (k0, c0, p0), (k1, c1, p1) = out
+    assert np.max(np.abs(k0 - k1)) <= 1
+    np.testing.assert_allclose(c1, c0, rtol=1e-8)
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7 * np.abs(p0).max())
+
+
 def test_full_size_cg_true_residual():
     from foto.synthetic import translating_gaussian
     Nt, Ny, Nx = 32, 480, 640
     rho0, rhoT = translating_gaussian(Nx, Ny)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=1) as s:
         s.iterate(1, 0.0, False)
         phi = s.phi()
         assert 100 < s.cg_its[0] < 1000
