@@ -230,13 +230,13 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rho0, rho0, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rhoT, rhoT, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
         FOTO_HIP_CHECK(launch_init_mu(s.g, s.rho0, s.rhoT, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->s));
-        if (c->o.cg_mode == 1) {
+        if (c->o.cg_mode == 1 || c->o.cg_mode == 2) {
             s.spec.reset(new SpectralPlan());
-            FOTO_TRY(s.spec->init(s.g, W, c->r, c->eps, c->s));
+            FOTO_TRY(s.spec->init(s.g, W, c->r, c->eps, c->o.cg_mode, c->s));
         }
         c->sh.push_back(std::move(sp));
     }
-    if (c->o.cg_mode == 1 && W > 1) {
+    if (c->o.cg_mode != 0 && W > 1) {
         set_error("spectral CG (cg_mode=1) is single-shard only in this build");
         return FOTO_ERR_ARG;
     }
@@ -298,7 +298,7 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
 // collective call sequence stays identical across ranks.
 static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
     const int maxiter = c->o.cg_maxiter;
-    if (c->o.cg_mode == 1) {
+    if (c->o.cg_mode != 0) {
         Shard& s = *c->sh[0];
         FOTO_TRY(s.spec->solve(s.rv, s.phi, c->o.cg_rtol, maxiter, c->last_cg, iters, info, &c->kt, c->s));
         c->last_cg = *iters;

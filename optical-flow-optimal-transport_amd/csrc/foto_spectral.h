@@ -7,7 +7,7 @@ namespace foto {
 struct KTimer;
 
 struct SpectralPlan {
-    int init(const Geo& g, int world, double r, double eps, hipStream_t s);
+    int init(const Geo& g, int world, double r, double eps, int sstep, hipStream_t s);
     // b (physical, overwritten as scratch) -> x (physical); scipy stopping rule.
     int solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info, KTimer* kt,
               hipStream_t s);

@@ -337,6 +337,189 @@ __global__ __launch_bounds__(NT) void k_spec_xhat(SpecTab T, const double* __res
     });
 }
 
+// ============================================================================ s-step (s = 2) CG in the eigenbasis
+//
+// One pass = two CG iterations.  State between passes: r = r_k, q = p_{k-1}.  The pass
+// applies the two steps pointwise (p = beta q + r; r -= alpha lam p; q = p -- exactly
+// scipy's per-element recurrence) with scalars prepared by the previous pass, then
+// accumulates the Chebyshev moments of the NEW state,
+//     M^rr_m = sum T_m(x) r^2,  M^rq_m = sum T_m(x) r q,  M^qq_m = sum T_m(x) q^2,
+//     x = (lam - c0) / c1 in [-1, 1],  m = 0..6,
+// from which the last block computes the next two iterations' rho, p.Ap, alpha, beta and
+// the stop test (r_{k+i} = A_i(lam) r + B_i(lam) q with Chebyshev-coefficient polynomials;
+// inner products through the Gram matrix (M_{a+c} + M_{|a-c|}) / 2).  s = 2 reproduces
+// scipy's iterates to rounding (s >= 3 loses digits to the basis conditioning; measured).
+
+constexpr int SM = 7;   // moments 0..6 (polynomial degree <= 3 per factor)
+
+struct SStep {
+    int k;        // iterations applied so far
+    int nsteps;   // steps the next pass applies (0, 1, 2)
+    int fin;      // after applying nsteps the solve is finished
+    int conv;     // ... because the stop test passed (else: maxiter reached)
+    int done;     // 1 converged, 2 maxiter reached (host polls this)
+    int iters;    // iterations at finish
+    double a[2], b[2];
+    double rho_prev;   // rho_{k-1}
+    double atol;
+    double c0, c1;
+};
+
+struct SPoly {   // (coefficients on T_a(x) r, coefficients on T_a(x) q), a = 0..3
+    double r[4], q[4];
+};
+
+__device__ __forceinline__ double gram(const double* M, int a, int c) {
+    return 0.5 * (M[a + c] + M[a > c ? a - c : c - a]);
+}
+
+__device__ double sp_ip(const SPoly& U, const SPoly& V, const double* Mrr, const double* Mrq, const double* Mqq) {
+    double s = 0.0;
+    for (int a = 0; a < 4; ++a)
+        for (int c = 0; c < 4; ++c) {
+            s += U.r[a] * V.r[c] * gram(Mrr, a, c);
+            s += U.r[a] * V.q[c] * gram(Mrq, a, c);
+            s += U.q[a] * V.r[c] * gram(Mrq, c, a);
+            s += U.q[a] * V.q[c] * gram(Mqq, a, c);
+        }
+    return s;
+}
+
+__device__ SPoly sp_mul_lam(const SPoly& U, double c0, double c1) {
+    SPoly Y;
+    auto one = [&](const double* c, double* y) {
+        double xc[4] = {0.0, 0.0, 0.0, 0.0};
+        xc[1] += c[0];
+        for (int m = 1; m < 3; ++m) { xc[m + 1] += 0.5 * c[m]; xc[m - 1] += 0.5 * c[m]; }
+        for (int m = 0; m < 4; ++m) y[m] = c0 * c[m] + c1 * xc[m];
+    };
+    one(U.r, Y.r);
+    one(U.q, Y.q);
+    return Y;
+}
+
+// next pass's scalars from the moments of (r_k, p_{k-1}); one thread.  scipy's loop:
+// top-of-iteration test ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p.
+__device__ void sstep2_plan(SStep& S, const double* Mrr, const double* Mrq, const double* Mqq, int maxiter) {
+    SPoly R = {{1.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    SPoly P = {{0.0, 0.0, 0.0, 0.0}, {1.0, 0.0, 0.0, 0.0}};
+    double rho_prev = S.rho_prev;
+    int n = 0;
+    bool conv = false;
+    for (int i = 0; i < 2 && S.k + i < maxiter; ++i) {
+        const double rho = (i == 0) ? Mrr[0] : sp_ip(R, R, Mrr, Mrq, Mqq);
+        if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
+        SPoly Pn;
+        double beta = 0.0;
+        if (S.k + i == 0) {
+            Pn = R;
+        } else {
+            beta = rho / rho_prev;
+            for (int m = 0; m < 4; ++m) { Pn.r[m] = beta * P.r[m] + R.r[m]; Pn.q[m] = beta * P.q[m] + R.q[m]; }
+        }
+        const SPoly Q = sp_mul_lam(Pn, S.c0, S.c1);
+        const double alpha = rho / sp_ip(Pn, Q, Mrr, Mrq, Mqq);
+        for (int m = 0; m < 4; ++m) { R.r[m] -= alpha * Q.r[m]; R.q[m] -= alpha * Q.q[m]; }
+        P = Pn;
+        rho_prev = rho;
+        S.a[i] = alpha;
+        S.b[i] = beta;
+        ++n;
+    }
+    S.nsteps = n;
+    S.rho_prev = rho_prev;
+    S.fin = 0;
+    S.conv = conv ? 1 : 0;
+    if (conv || S.k + n >= maxiter) {
+        S.fin = 1;
+        S.iters = conv ? S.k + n : maxiter;
+        if (n == 0) S.done = conv ? 1 : 2;   // nothing left to apply
+    }
+}
+
+__device__ __forceinline__ void cheb7(double x, double* T) {
+    T[0] = 1.0;
+    T[1] = x;
+#pragma unroll
+    for (int m = 2; m < SM; ++m) T[m] = 2.0 * x * T[m - 1] - T[m - 2];
+}
+
+template <bool VEC, bool INIT>
+__global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
+                                                const double* __restrict__ bh, SStep* Sg, RedBuf rb,
+                                                double rtol, int maxiter) {
+    __shared__ SStep SS;
+    if (threadIdx.x == 0) SS = *Sg;
+    __syncthreads();
+    if (!INIT && (SS.done || SS.nsteps == 0)) return;
+    const int k = SS.k, ns = SS.nsteps;
+    const double a0 = SS.a[0], b0 = SS.b[0], a1 = SS.a[1], b1 = SS.b[1];
+    const double c0 = SS.c0, ic1 = 1.0 / SS.c1;
+    double acc[3 * SM];
+#pragma unroll
+    for (int m = 0; m < 3 * SM; ++m) acc[m] = 0.0;
+    auto moments = [&](double lam, double r, double q) {
+        double Tm[SM];
+        cheb7((lam - c0) * ic1, Tm);
+        const double rr = r * r, rq = r * q, qq = q * q;
+#pragma unroll
+        for (int m = 0; m < SM; ++m) {
+            acc[m] += Tm[m] * rr;
+            acc[SM + m] += Tm[m] * rq;
+            acc[2 * SM + m] += Tm[m] * qq;
+        }
+    };
+    spec_for_each(T, [&](int64_t i, double l0, double l1, int n2) {
+        double r0, r1, q0 = 0.0, q1 = 0.0;
+        if (INIT) {
+            ld2<VEC>(bh, i, n2, r0, r1);
+            st2<VEC>(rh, i, n2, r0, r1);
+        } else {
+            ld2<VEC>(rh, i, n2, r0, r1);
+            if (k > 0) ld2<VEC>(ph, i, n2, q0, q1);
+            // step 0 (iteration k)
+            double p0 = (k == 0) ? r0 : b0 * q0 + r0;
+            double p1 = (k == 0) ? r1 : b0 * q1 + r1;
+            r0 = r0 - a0 * (l0 * p0);
+            r1 = r1 - a0 * (l1 * p1);
+            q0 = p0;
+            q1 = p1;
+            if (ns == 2) {   // step 1 (iteration k + 1)
+                p0 = b1 * q0 + r0;
+                p1 = b1 * q1 + r1;
+                r0 = r0 - a1 * (l0 * p0);
+                r1 = r1 - a1 * (l1 * p1);
+                q0 = p0;
+                q1 = p1;
+            }
+            st2<VEC>(rh, i, n2, r0, r1);
+            st2<VEC>(ph, i, n2, q0, q1);
+        }
+        moments(l0, r0, q0);
+        if (n2 == 2) moments(l1, r1, q1);
+    });
+    double tot[3 * SM];
+    if (sp_reduce_last<3 * SM>(acc, rb, tot) && threadIdx.x == 0) {
+        SStep S = SS;
+        if (INIT) {
+            S.k = 0;
+            S.rho_prev = 0.0;
+            S.atol = fmax(0.0, rtol * sqrt(tot[0]));   // scipy: max(atol, rtol * ||b||)
+            S.done = 0;
+        } else {
+            S.k = k + ns;
+            if (S.fin) {
+                S.done = S.conv ? 1 : 2;
+                S.nsteps = 0;
+                *Sg = S;
+                return;
+            }
+        }
+        sstep2_plan(S, tot, tot + SM, tot + 2 * SM, maxiter);
+        *Sg = S;
+    }
+}
+
 // ============================================================================ plan
 
 struct SpecImpl {
@@ -349,6 +532,10 @@ struct SpecImpl {
     double* gath = nullptr;
     CGScal* S = nullptr;
     CGScal* hS = nullptr;
+    SStep* S2 = nullptr;
+    SStep* hS2 = nullptr;
+    int nblocks2 = 0;
+    int sstep = 1;
     std::vector<void*> allocs;
     int nblocks = 0;
 
@@ -360,6 +547,7 @@ struct SpecImpl {
     ~SpecImpl() {
         for (void* p : allocs) (void)hipFree(p);
         if (hS) (void)hipHostFree(hS);
+        if (hS2) (void)hipHostFree(hS2);
     }
     SpecTab tab() const {
         SpecTab T;
@@ -386,7 +574,11 @@ static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, s
     }
 }
 
-int SpectralPlan::init(const Geo& g, int world, double r, double eps, hipStream_t s) {
+int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep, hipStream_t s) {
+    if (sstep != 1 && sstep != 2) {
+        set_error("spectral CG: s-step must be 1 or 2");
+        return FOTO_ERR_ARG;
+    }
     if (world != 1 || g.nloc != g.Nt) {
         set_error("spectral CG needs the whole time axis on one shard");
         return FOTO_ERR_ARG;
@@ -397,6 +589,7 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, hipStream_
     }
     auto* P = new SpecImpl();
     impl = P;
+    P->sstep = sstep;
     P->g = g;
     P->r = r;
     P->eps = eps;
@@ -424,14 +617,18 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, hipStream_
     const int rows = g.Nt * g.Ny;
     const int ntiles = ((g.Nx + 127) / 128) * ((rows + 3) / 4);
     P->nblocks = std::min(ntiles, 2048);
-    FOTO_TRY(P->alloc(sizeof(double) * (2 * P->nblocks + 8), &b));
+    P->nblocks2 = std::min(ntiles, 512);
+    const int cap = std::max(2 * P->nblocks, 3 * SM * P->nblocks2);
+    FOTO_TRY(P->alloc(sizeof(double) * (cap + 8), &b));
     P->rb.partials = (double*)b;
-    P->rb.ticket = (unsigned*)((double*)b + 2 * P->nblocks);
-    P->rb.cap = 2 * P->nblocks;
+    P->rb.ticket = (unsigned*)((double*)b + cap);
+    P->rb.cap = cap;
     FOTO_HIP_CHECK(hipMemset(P->rb.ticket, 0, 8 * sizeof(double)));
     FOTO_TRY(P->alloc(sizeof(double) * 4, &b)); P->gath = (double*)b;
     FOTO_TRY(P->alloc(sizeof(CGScal), &b)); P->S = (CGScal*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
+    FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS2, sizeof(SStep)));
     (void)s;
     return 0;
 }
@@ -463,6 +660,51 @@ static int inverse3(SpecImpl* P, double* in, double* scratch, double* out, KTime
     return 0;
 }
 
+static int solve_s2(SpecImpl* P, const SpecTab& T, bool vec, double rtol, int maxiter, int predicted, int* iters,
+                    int* info, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    SStep h{};
+    std::vector<double> mt(g.Nt), my(g.Ny), mx(g.Nx);
+    FOTO_HIP_CHECK(hipMemcpy(mt.data() + g.Nt - 1, P->mt + g.Nt - 1, 8, hipMemcpyDeviceToHost));
+    FOTO_HIP_CHECK(hipMemcpy(my.data() + g.Ny - 1, P->my + g.Ny - 1, 8, hipMemcpyDeviceToHost));
+    FOTO_HIP_CHECK(hipMemcpy(mx.data() + g.Nx - 1, P->mx + g.Nx - 1, 8, hipMemcpyDeviceToHost));
+    const double lmin = T.reps, lmax = T.reps + T.r * (mt[g.Nt - 1] + my[g.Ny - 1] + mx[g.Nx - 1]);
+    h.c0 = 0.5 * (lmax + lmin);
+    h.c1 = 0.5 * (lmax - lmin);
+    *P->hS2 = h;
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->S2, P->hS2, sizeof(SStep), hipMemcpyHostToDevice, s));
+    {
+        hipEvent_t e = kt ? kt->start(s) : nullptr;
+        if (vec) k_spec_s2<true, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
+        else k_spec_s2<false, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
+        FOTO_HIP_CHECK(hipGetLastError());
+        if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * N);
+    }
+    int passes = 0;
+    const int first = predicted > 6 ? (predicted - 4) / 2 : 4;
+    while (true) {
+        const int chunk = (passes == 0) ? first : 1;
+        for (int j = 0; j < chunk; ++j, ++passes) {
+            hipEvent_t e = kt ? kt->start(s) : nullptr;
+            if (vec) k_spec_s2<true, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
+            else k_spec_s2<false, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
+            FOTO_HIP_CHECK(hipGetLastError());
+            if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * N);
+        }
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        if (P->hS2->done) break;
+        if (passes > maxiter + 4) {
+            set_error("spectral s-step CG did not terminate");
+            return FOTO_ERR_STATE;
+        }
+    }
+    *iters = P->hS2->iters;
+    *info = (P->hS2->done == 1) ? 0 : maxiter;
+    return 0;
+}
+
 int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info,
                         KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
@@ -475,6 +717,14 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     if (vec) k_spec_init<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
     else k_spec_init<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
     FOTO_HIP_CHECK(hipGetLastError());
+    if (P->sstep == 2) {
+        FOTO_TRY(solve_s2(P, T, vec, rtol, maxiter, predicted, iters, info, kt, s));
+        if (vec) k_spec_xhat<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+        else k_spec_xhat<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_TRY(inverse3(P, P->tmp, b, x, kt, s));
+        return 0;
+    }
     FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
     int k = 0;
     bool done = false;

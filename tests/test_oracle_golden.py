@@ -172,3 +172,20 @@ def test_gn(gold):
         u, v, m = O.gn_solve(f1, f2, w, h, alpha, lam)
         for a, ref in ((u, d[f"n{g}_u"]), (v, d[f"n{g}_v"]), (m, d[f"n{g}_m"])):
             np.testing.assert_allclose(a, ref, rtol=0, atol=1e-8)
+
+
+@pytest.mark.slow
+def test_reference_rounding_sensitivity(gold):
+    """Documents the parity bar of the full solve: changing only the rounding of A p
+    (matrix-free stencil instead of scipy CSR) moves CG counts by one and crit by ~1e-6
+    relative in the reference algorithm itself."""
+    d = gold("bb_c1.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    st = {}
+    u, v, m = O.solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps,
+                      max_it=int(max_it), stats=st, log=lambda s: None, assembled=False)
+    dk = np.abs(np.array(st["cg_its"]) - d["cg_its"])
+    rel = np.max(np.abs(st["crit"] / d["crit"] - 1))
+    assert dk.max() <= 1 and 1e-7 < rel < 1e-5
+    assert np.abs(u - d["u"]).max() < 1e-5
