@@ -36,7 +36,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "0")))
+    ap.add_argument("--cg-mode", type=int, default=None,
+                    help="0 stencil CG (time-sharded multi-GPU path), 1 spectral CG, 2 spectral s-step CG "
+                         "(default: 2 on one GPU, 0 when sharded)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -89,6 +91,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.cg_mode is None:
+        args.cg_mode = int(os.environ.get("FOTO_CG_MODE", "2" if world == 1 else "0"))
     dist = None
     nccl_id = None
     if world > 1:
@@ -148,7 +152,7 @@ def main():
             kern[name] = {"launches": k["n"], "avg_us": 1e3 * k["ms"] / max(k["n"], 1),
                           "avg_gbs": (k["bytes"] / max(k["n"], 1)) / (1e-3 * k["ms"] / max(k["n"], 1)) / 1e9
                           if k["ms"] > 0 else None}
-        dom = "spec_cg" if args.cg_mode == 1 else "cg_upd"
+        dom = "spec_cg" if args.cg_mode != 0 else "cg_upd"
         if dom in kst and kst[dom]["ms"] > 0:
             k = kst[dom]
             avg_s = 1e-3 * k["ms"] / k["n"]
@@ -182,7 +186,7 @@ def main():
             "data": "synthetic (translating Gaussian pair, SURVEY.md §8(d); no Middlebury offline)",
             "config": {"workload": "FOTO Benamou-Brenier outer iteration, 640x480x32, r=1, eps=1e-2, "
                                    "CG rtol=1e-6 (scipy rule), stop rules off",
-                       "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral"][args.cg_mode],
+                       "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral-cg", "spectral-sstep2"][args.cg_mode],
                        "parallelism": f"time-slab x{world}" if world > 1 else "single GPU"},
             "cg_iters_per_step": round(float(np.mean(cg_steps)), 2) if cg_steps else None,
             "cg_iters_per_s": round(float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,

@@ -714,9 +714,6 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     // b (physical) -> b^ ; b is scratch afterwards
     const bool vec = (g.Nx % 2) == 0;
     FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
-    if (vec) k_spec_init<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
-    else k_spec_init<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
-    FOTO_HIP_CHECK(hipGetLastError());
     if (P->sstep == 2) {
         FOTO_TRY(solve_s2(P, T, vec, rtol, maxiter, predicted, iters, info, kt, s));
         if (vec) k_spec_xhat<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
@@ -725,6 +722,9 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
         FOTO_TRY(inverse3(P, P->tmp, b, x, kt, s));
         return 0;
     }
+    if (vec) k_spec_init<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
+    else k_spec_init<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->rb, P->gath);
+    FOTO_HIP_CHECK(hipGetLastError());
     FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
     int k = 0;
     bool done = false;
