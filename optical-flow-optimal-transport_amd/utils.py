@@ -1,0 +1,117 @@
+"""Drop-in for the reference's ``utils.py``.
+
+Hot path (GPU, libfoto.so):
+  opticalflow_from_benamoubrenier  utils.py:148-183 -> foto_flow_from_phi (one thread per
+                                   pixel walks the Nt-1 trajectory steps, then m = -div_D)
+Host utilities (image / .flo IO and evaluation metrics):
+  openGrayscaleImage, reconstructTrajectory (single start point), apply_opticalflow,
+  openFlo, saveFlo, EE, AE, IE -- same semantics and quirks as utils.py:25-354
+  (vectorised over pixels instead of Python loops).
+"""
+import math  # noqa: F401  (kept for API parity with the reference module)
+
+import numpy as np
+from PIL import Image
+
+from foto import ops as _ops
+
+
+def openGrayscaleImage(inputPathname):
+    """8-bit grayscale -> flat float64 in [0, 1], width, height (utils.py:25-42)."""
+    f = np.asarray(Image.open(inputPathname).convert("L"))
+    h, w = f.shape
+    return f.reshape(-1) / 255, w, h
+
+
+def reconstructTrajectory(xStart, yStart, u, v, Nx, Ny, Nt):
+    """One particle through the (Nt x Nx*Ny) velocity slabs u, v with clamped bilinear
+    interpolation (utils.py:44-99).  Host helper for a single start point; the solver
+    integrates all pixels on the GPU (opticalflow_from_benamoubrenier)."""
+    x, y = xStart, yStart
+    for n in range(Nt - 1):
+        tx = max(0, min(Nx - 2, int(x)))
+        ty = max(0, min(Ny - 2, int(y)))
+        dX, dY = x - tx, y - ty
+        w1, w2, w3, w4 = (1 - dY) * (1 - dX), dX * (1 - dY), dY * dX, (1 - dX) * dY
+        a, b = ty * Nx + tx, (ty + 1) * Nx + tx
+        x += w1 * u[n, a] + w2 * u[n, a + 1] + w3 * u[n, b + 1] + w4 * u[n, b]
+        y += w1 * v[n, a] + w2 * v[n, a + 1] + w3 * v[n, b + 1] + w4 * v[n, b]
+    return [x - xStart, y - yStart]
+
+
+def opticalflow_from_benamoubrenier(phi, Nt, Nx, Ny, grad=None, div=None):
+    """(u, v, m) from the space-time potential phi (utils.py:148-183), on the GPU.
+    ``grad``/``div`` are accepted for signature parity; the kernels implement the
+    reference's operators.grad(bc='N') and operators.div(bc='D')."""
+    return _ops.flow_from_phi(phi, Nt, Nx, Ny)
+
+
+def apply_opticalflow(f1, u, v, w, h, m=np.array([None])):
+    """Backward bilinear warp of (1+m) f1 by (u, v) with the reference's edge handling
+    (utils.py:186-248): weights from the unclamped fractional parts, indices clamped to
+    the image, the +1 neighbour collapsed onto the edge pixel on the last row / column."""
+    if m.all() != None:  # noqa: E711  -- reference quirk: true for every numeric m
+        f1 = (1 + m) * f1
+    f1 = np.asarray(f1, dtype=np.float64)
+    ii, jj = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
+    ti = ii.ravel() - np.asarray(v, dtype=np.float64)
+    tj = jj.ravel() - np.asarray(u, dtype=np.float64)
+    dI = ti - np.trunc(ti)
+    dJ = tj - np.trunc(tj)
+    w1, w2, w3, w4 = (1 - dI) * (1 - dJ), dJ * (1 - dI), dI * dJ, (1 - dJ) * dI
+    ti = np.where(ti >= h, h - 1, ti)
+    tj = np.where(tj >= w, w - 1, tj)
+    ti = np.where(ti < 0, 0, ti)
+    tj = np.where(tj < 0, 0, tj)
+    a = ti.astype(np.int64)
+    b = tj.astype(np.int64)
+    a1 = np.where(a < h - 1, a + 1, a)
+    b1 = np.where(b < w - 1, b + 1, b)
+    x = w1 * f1[a * w + b]
+    x = x + w2 * f1[a * w + b1]
+    x = x + w3 * f1[a1 * w + b1]
+    x = x + w4 * f1[a1 * w + b]
+    return x
+
+
+def openFlo(pathname):
+    """Middlebury .flo reader -> (w, h, u, v) (utils.py:250-271)."""
+    with open(pathname, "rb") as f:
+        magic = np.fromfile(f, np.float32, count=1)[0]
+        if 202021.25 != magic:
+            print("Magic number incorrect. Invalid .flo file")
+        w = np.fromfile(f, np.int32, count=1)[0]
+        h = np.fromfile(f, np.int32, count=1)[0]
+        data = np.fromfile(f, np.float32)
+    data = data.reshape(h, w, 2)
+    return w, h, data[..., 0].flatten(), data[..., 1].flatten()
+
+
+def saveFlo(w, h, u, v, pathname):
+    """Middlebury .flo writer: float32 magic, int32 w, h, interleaved float32 (u, v)
+    (utils.py:273-292)."""
+    with open(pathname, "wb") as f:
+        np.array([202021.25], dtype=np.float32).tofile(f)
+        np.array([w, h], dtype=np.int32).tofile(f)
+        np.stack([np.asarray(u, dtype=np.float64), np.asarray(v, dtype=np.float64)], axis=1).astype(np.float32).tofile(f)
+
+
+def EE(w, h, u, v, uGT, vGT):
+    """Average endpoint error and its std over pixels with EE <= 50 (utils.py:294-315)."""
+    e = np.sqrt((u - uGT) ** 2 + (v - vGT) ** 2)[: w * h]
+    kept = e[e <= 50]
+    mean = np.sum(kept) / len(kept)
+    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+
+
+def AE(w, h, u, v, uGT, vGT):
+    """Average angular error (radians) and std, NaNs ignored (utils.py:317-338)."""
+    a = np.arccos((1.0 + u * uGT + v * vGT) / (np.sqrt(1.0 + u ** 2 + v ** 2) * np.sqrt(1.0 + uGT ** 2 + vGT ** 2)))
+    kept = a[: w * h][~np.isnan(a[: w * h])]
+    mean = np.sum(kept) / len(kept)
+    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+
+
+def IE(w, h, I, IGT):
+    """RMS intensity error on the 0..255 scale (utils.py:340-354)."""
+    return np.sqrt(np.sum((255 * I - 255 * IGT) ** 2) / (w * h))

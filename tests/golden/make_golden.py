@@ -20,6 +20,7 @@ Cases (SURVEY.md §8(c) "Golden vectors to generate"):
                  eps=1e-2, max_it=100) -- 46 outer iterations, ~25 s
   gn.npz         GLLOpticalFlow assemble A@x, b, process() u, v, m on 40x30 and 17x13
   io.npz         saveFlo bytes, openFlo round trip, EE/AE/IE, apply_opticalflow
+  cli.npz        main.py's pipeline on a 36x28 PNG pair (FOTO Nt=4, 8 its; GN): flows, IE, .flo bytes
 """
 import argparse
 import contextlib
@@ -268,6 +269,44 @@ def gen_io(utils, rng):
          uGT=uGT, vGT=vGT, ee=ee, ae=ae, rec=rec, ie=ie)
 
 
+def gen_cli(utils, bb, classical):
+    """The computation main.py performs (main.py:52-146), reproduced by calling the
+    reference functions directly (main.py itself imports cv2, absent here): PNG frames ->
+    openGrayscaleImage -> solver -> apply_opticalflow / clip / IE -> saveFlo bytes."""
+    from PIL import Image
+    w, h = 36, 28
+    a, b = textured_pair(w, h, seed=11, dx=1.2, dy=0.6)
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        p0, p1 = os.path.join(d, "f0.png"), os.path.join(d, "f1.png")
+        Image.fromarray(np.uint8(np.round(255 * a.reshape(h, w))), "L").save(p0)
+        Image.fromarray(np.uint8(np.round(255 * b.reshape(h, w))), "L").save(p1)
+        out["png0"] = np.fromfile(p0, dtype=np.uint8)
+        out["png1"] = np.fromfile(p1, dtype=np.uint8)
+        f1, w_, h_ = utils.openGrayscaleImage(p0)
+        f2, _, _ = utils.openGrayscaleImage(p1)
+        for algo in ("foto", "GN"):
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                if algo == "foto":
+                    u, v, m = bb.solve(f1, f2, 4, w_, h_, r=1.0, convergence_tol=0.01, reg_epsilon=1e-2, max_it=8)
+                else:
+                    g = classical.GLLOpticalFlow(w_, h_)
+                    g.setAlpha(0.1)
+                    g.setLambda(0.2)
+                    u, v, m = g.assemble(f1, f2).process()
+            rec = np.clip(utils.apply_opticalflow(f1, u, v, w_, h_, m), 0, 1)
+            ie = utils.IE(w_, h_, rec, f2)
+            fp = os.path.join(d, algo + ".flo")
+            utils.saveFlo(w_, h_, u, v, fp)
+            out[f"{algo}_u"], out[f"{algo}_v"], out[f"{algo}_m"] = np.asarray(u), np.asarray(v), np.asarray(m)
+            out[f"{algo}_rec"], out[f"{algo}_ie"] = rec, np.array(ie)
+            out[f"{algo}_flo"] = np.fromfile(fp, dtype=np.uint8)
+            out[f"{algo}_stdout"] = np.array(buf.getvalue())
+    out["f1"], out["f2"] = f1, f2
+    save("cli.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -287,6 +326,7 @@ def main():
     gen_flow(utils, operators, rng)
     gen_gn(classical, rng)
     gen_io(utils, rng)
+    gen_cli(utils, bb, classical)
     gen_bb(bb, "bb_small.npz", 4, 20, 16, r=1, convergence_tol=0.01, reg_epsilon=1e-2, max_it=30)
     gen_bb(bb, "bb_tex.npz", 5, 24, 18, pair="tex", r=1.5, convergence_tol=0.05, reg_epsilon=1e-3, max_it=12)
     if not args.skip_c1:
