@@ -76,7 +76,9 @@ typedef struct {
     int device;           /* HIP device ordinal; -1 = current device                       */
     int cg_maxiter;       /* 1000 (benamou_brenier.py:85)                                  */
     double cg_rtol;       /* 1e-6 (benamou_brenier.py:85)                                  */
-    int cg_mode;          /* 0 = stencil CG (7-point matvec), 1 = spectral CG (DCT basis)  */
+    int cg_mode;          /* 0 = stencil CG (7-point matvec), 1 = spectral CG (DCT-II      */
+                          /* eigenbasis, one pass / iteration), 2 = spectral s-step CG     */
+                          /* (one pass / two iterations); spectral needs world == 1        */
     int rank, world;      /* time-slab sharding over `world` processes (RCCL); 1 = single  */
     const void* nccl_id;  /* 128-byte ncclUniqueId (foto_nccl_unique_id on rank 0)         */
     int virtual_ranks;    /* >1: shard over this many in-process slabs on ONE device       */
@@ -113,8 +115,8 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
                    double reg_epsilon, const foto_bb_opts* opts, foto_bb_ctx** out);
 /* Run up to `max_iters` outer iterations (stepA + stepB + stepC + criterion).  With
  * use_stop_rules = 1 it stops like the reference (crit <= tol, or |dcrit| < 1e-5).
- * `total_max_it` is the max_it printed by the reference's "(i/max_it)" line and
- * passed to cb only for numbering.  Returns 1 if a stop rule fired, 0 otherwise.  */
+ * cb (may be NULL) gets (iteration index, crit, CG iterations, CG info) after each
+ * outer iteration.  Returns 1 if a stop rule fired, 0 otherwise, < 0 on error.    */
 int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double convergence_tol, int use_stop_rules,
                     foto_bb_iter_cb cb, void* user, int* iters_done);
 /* Flow (u, v, m) from the last phi: utils.opticalflow_from_benamoubrenier.
