@@ -1,0 +1,295 @@
+"""Multi-process checks of the time-sharded path on CPU (gloo, world sizes 2 and 3).
+
+libfoto's sharded solver (csrc/foto_bb.cpp) decomposes the space-time grid into contiguous
+time slabs with one halo plane per side, exchanges halos before every stencil application,
+all-gathers per-rank dot-product partials and sums them in rank order, and relays the
+trajectory positions rank to rank for the flow.  Here the same decomposition is executed
+with numpy on each rank and torch.distributed (gloo) as the transport, and must reproduce
+the single-process oracle: identical CG counts, same crit / phi / flow to 1e-9.  The
+rendezvous used by bench.py (RCCL unique-id broadcast, barrier, max-over-ranks timing) is
+exercised as well.  The GPU-side counterpart (virtual ranks on one device) is
+tests/test_gpu_parity.py::test_bb_virtual_ranks_match_single.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def split_planes(Nt, W, rank):
+    """csrc/foto_bb.cpp split_planes: balanced contiguous slabs."""
+    base, extra = divmod(Nt, W)
+    nloc = base + (1 if rank < extra else 0)
+    t0 = rank * base + min(rank, extra)
+    return t0, nloc
+
+
+class Shard:
+    def __init__(self, rank, W, Nt, Ny, Nx):
+        self.rank, self.W, self.Nt, self.Ny, self.Nx = rank, W, Nt, Ny, Nx
+        self.t0, self.nloc = split_planes(Nt, W, rank)
+
+    # ------------------------------------------------------------ halo exchange of (nloc+2, Ny, Nx)
+    def halo(self, a):
+        reqs = []
+        lo, hi = self.rank - 1, self.rank + 1
+        recv_lo = torch.zeros(self.Ny, self.Nx, dtype=torch.float64)
+        recv_hi = torch.zeros(self.Ny, self.Nx, dtype=torch.float64)
+        if lo >= 0:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[1])), lo))
+            reqs.append(dist.irecv(recv_lo, lo))
+        if hi < self.W:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[self.nloc])), hi))
+            reqs.append(dist.irecv(recv_hi, hi))
+        for r in reqs:
+            r.wait()
+        if lo >= 0:
+            a[0] = recv_lo.numpy()
+        if hi < self.W:
+            a[self.nloc + 1] = recv_hi.numpy()
+
+    def allsum(self, *vals):
+        """all-gather per-rank partials, sum in rank order (identical on every rank)."""
+        t = torch.tensor(vals, dtype=torch.float64)
+        out = [torch.zeros_like(t) for _ in range(self.W)]
+        dist.all_gather(out, t)
+        tot = np.zeros(len(vals))
+        for g in range(self.W):
+            tot = tot + out[g].numpy()
+        return tot
+
+    # ------------------------------------------------------------ local operators (global t aware)
+    def lap(self, e):
+        """L_st on the local planes of the halo-extended field e (nloc+2, Ny, Nx)."""
+        from oracle import foto_oracle as O
+        P = e[1:-1]
+        out = O.d1_lap(P, 1) + O.d1_lap(P, 2)
+        for l in range(self.nloc):
+            t = self.t0 + l
+            s = np.zeros_like(P[l])
+            if t > 0:
+                s += e[l] - P[l]
+            if t < self.Nt - 1:
+                s += e[l + 2] - P[l]
+            out[l] += s
+        return out
+
+    def grad_t(self, e):
+        P = e[1:-1]
+        out = np.empty_like(P)
+        for l in range(self.nloc):
+            t = self.t0 + l
+            if t == 0:
+                out[l] = e[l + 2] - P[l]
+            elif t == self.Nt - 1:
+                out[l] = P[l] - e[l]
+            else:
+                out[l] = 0.5 * (e[l + 2] - e[l])
+        return out
+
+    def ext(self, a):
+        e = np.zeros((self.nloc + 2, self.Ny, self.Nx))
+        e[1:-1] = a
+        return e
+
+
+def sharded_cg(S, F, r, eps, rtol=1e-6, maxiter=1000):
+    """scipy's CG on the shard: halo of p before A p, dot products via allsum."""
+    bb = S.allsum(float(np.sum(F * F)))[0]
+    atol = rtol * np.sqrt(bb)
+    x = np.zeros_like(F)
+    rv = F.copy()
+    p = None
+    rho_prev = None
+    if bb == 0:
+        return x, 0
+    for k in range(maxiter):
+        rho = S.allsum(float(np.sum(rv * rv)))[0]
+        if np.sqrt(rho) < atol:
+            return x, k
+        p = rv.copy() if k == 0 else (rho / rho_prev) * p + rv
+        e = S.ext(p)
+        S.halo(e)
+        q = -r * S.lap(e) + (r * eps) * p
+        alpha = rho / S.allsum(float(np.sum(p * q)))[0]
+        x = x + alpha * p
+        rv = rv - alpha * q
+        rho_prev = rho
+    return x, maxiter
+
+
+def sharded_outer(S, mu, q, rho0, rhoT, r, eps):
+    from oracle import foto_oracle as O
+    Nt, Ny, Nx = S.Nt, S.Ny, S.Nx
+    # RHS: needs halos of mu_t - r q_t
+    wt = S.ext(mu[0] - r * q[0])
+    S.halo(wt)
+    F = S.grad_t(wt) + O.d1_central_weird(mu[1] - r * q[1], 2) + O.d1_central_weird(mu[2] - r * q[2], 1)
+    if S.t0 == 0:
+        F[0] -= (rho0 - mu[0][0]) + r * q[0][0]
+    if S.t0 + S.nloc == Nt:
+        F[-1] += (rhoT - mu[0][-1]) + r * q[0][-1]
+    phi, its = sharded_cg(S, F, r, eps)
+    e = S.ext(phi)
+    S.halo(e)
+    gt = S.grad_t(e)
+    gx = O.d1_central_weird(phi, 2)
+    gy = O.d1_central_weird(phi, 1)
+    n = phi.size
+    pr = np.concatenate([(gt + mu[0] / r).ravel(), (gx + mu[1] / r).ravel(), (gy + mu[2] / r).ravel()])
+    qq = O.stepB(pr, n)
+    qn = [qq[:n].reshape(phi.shape), qq[n:2 * n].reshape(phi.shape), qq[2 * n:].reshape(phi.shape)]
+    mun = [mu[0] + r * (gt - qn[0]), mu[1] + r * (gx - qn[1]), mu[2] + r * (gy - qn[2])]
+    mun[0] = np.maximum(mun[0], 0)
+    gg = gx ** 2 + gy ** 2
+    num, den = S.allsum(float(np.sum(mun[0] * np.abs(gt + 0.5 * gg))), float(np.sum(mun[0] * gg)))
+    return mun, qn, phi, its, np.sqrt(num / (den + 1e-10))
+
+
+def sharded_flow(S, phi):
+    """trajectory relay: positions travel rank -> rank + 1; last rank finishes (u, v, m)."""
+    from oracle import foto_oracle as O
+    Nt, Ny, Nx = S.Nt, S.Ny, S.Nx
+    nxy = Nx * Ny
+    jj, ii = np.meshgrid(np.arange(Ny), np.arange(Nx), indexing="ij")
+    x0, y0 = ii.ravel().astype(float), jj.ravel().astype(float)
+    if S.rank == 0:
+        x, y = x0.copy(), y0.copy()
+    else:
+        buf = torch.zeros(2, nxy, dtype=torch.float64)
+        dist.recv(buf, S.rank - 1)
+        x, y = buf[0].numpy().copy(), buf[1].numpy().copy()
+    for n in range(S.t0, min(S.t0 + S.nloc, Nt - 1)):
+        g = O.grad2_central(phi[n - S.t0].ravel(), Nx, Ny, "N")
+        un, vn = g[:nxy], g[nxy:]
+        tx = np.clip(np.trunc(x), 0, Nx - 2).astype(np.int64)
+        ty = np.clip(np.trunc(y), 0, Ny - 2).astype(np.int64)
+        dX, dY = x - tx, y - ty
+        w1, w2, w3, w4 = (1 - dY) * (1 - dX), dX * (1 - dY), dY * dX, (1 - dX) * dY
+        a, b = ty * Nx + tx, (ty + 1) * Nx + tx
+        x = x + (w1 * un[a] + w2 * un[a + 1] + w3 * un[b + 1] + w4 * un[b])
+        y = y + (w1 * vn[a] + w2 * vn[a + 1] + w3 * vn[b + 1] + w4 * vn[b])
+    if S.rank < S.W - 1:
+        dist.send(torch.from_numpy(np.stack([x, y])), S.rank + 1)
+        return None
+    u, v = x - x0, y - y0
+    return u, v, -O.div2_central(np.concatenate([u, v]), Nx, Ny, "D")
+
+
+def _worker(rank, W, port, q, case):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "optical-flow-optimal-transport_amd"))
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=W)
+    try:
+        from foto.synthetic import textured_pair
+        Nt, Ny, Nx, r, eps, iters = case
+        rho0, rhoT = textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+        S = Shard(rank, W, Nt, Ny, Nx)
+        t = np.arange(S.t0, S.t0 + S.nloc)[:, None, None] / (Nt - 1)
+        mu = [(1 - t) * rho0.reshape(Ny, Nx) + t * rhoT.reshape(Ny, Nx), np.zeros((S.nloc, Ny, Nx)),
+              np.zeros((S.nloc, Ny, Nx))]
+        qv = [np.zeros((S.nloc, Ny, Nx)) for _ in range(3)]
+        crits, its = [], []
+        for _ in range(iters):
+            mu, qv, phi, k, crit = sharded_outer(S, mu, qv, rho0.reshape(Ny, Nx), rhoT.reshape(Ny, Nx), r, eps)
+            crits.append(crit)
+            its.append(k)
+        flow = sharded_flow(S, phi)
+        parts = [torch.zeros(Nt * Ny * Nx, dtype=torch.float64) for _ in range(W)]
+        mine = torch.zeros(Nt * Ny * Nx, dtype=torch.float64)
+        mine[S.t0 * Ny * Nx:(S.t0 + S.nloc) * Ny * Nx] = torch.from_numpy(phi.ravel())
+        dist.all_gather(parts, mine)
+        if flow is not None:
+            q.put(("flow", [np.asarray(a) for a in flow]))
+        if rank == 0:
+            q.put(("res", crits, its, sum(p.numpy() for p in parts)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_sharded_solver_matches_oracle(W):
+    sys.path.insert(0, REPO)
+    from oracle import foto_oracle as O
+    from foto.synthetic import textured_pair
+    case = (5, 18, 24, 1.5, 1e-3, 4)
+    Nt, Ny, Nx, r, eps, iters = case
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(g, W, port, q, case)) for g in range(W)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        item = q.get(timeout=300)
+        got[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    crits, its, phi = got["res"]
+    (u, v, m), = got["flow"]
+    rho0, rhoT = textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+    st = {}
+    uo, vo, mo = O.solve(rho0, rhoT, Nt, Nx, Ny, r=r, convergence_tol=0.0, reg_epsilon=eps, max_it=iters, stats=st,
+                         log=lambda s: None, assembled=False, stop_rules=False)
+    assert list(its) == list(st["cg_its"])
+    np.testing.assert_allclose(crits, st["crit"], rtol=1e-9)
+    np.testing.assert_allclose(phi, st["phi"], rtol=0, atol=1e-9 * np.abs(st["phi"]).max())
+    for a, b in ((u, uo), (v, vo), (m, mo)):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-9)
+
+
+def _rdv_worker(rank, W, port, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=W)
+    obj = [os.urandom(128) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)   # bench.py: RCCL unique id from rank 0
+    t = torch.tensor([0.5 + rank], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)   # bench.py: max-over-ranks timing
+    dist.barrier()
+    q.put((rank, obj[0], float(t.item())))
+    dist.destroy_process_group()
+
+
+def test_bench_rendezvous_gloo():
+    W = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rdv_worker, args=(g, W, port, q)) for g in range(W)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(W)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ids = {r[1] for r in res}
+    assert len(ids) == 1 and len(next(iter(ids))) == 128
+    assert all(r[2] == 0.5 + (W - 1) for r in res)
+
+
+def test_split_planes_matches_library_rule():
+    for Nt in (2, 5, 32, 64):
+        for W in range(1, min(Nt, 8) + 1):
+            spans = [split_planes(Nt, W, g) for g in range(W)]
+            assert spans[0][0] == 0 and sum(n for _, n in spans) == Nt
+            assert all(spans[g][0] + spans[g][1] == spans[g + 1][0] for g in range(W - 1))
+            assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
