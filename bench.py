@@ -36,9 +36,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cg-mode", type=int, default=None,
-                    help="0 stencil CG (time-sharded multi-GPU path), 1 spectral CG, 2 spectral s-step CG "
-                         "(default: 2 on one GPU, 0 when sharded)")
+    ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "2")),
+                    help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -91,8 +90,6 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.cg_mode is None:
-        args.cg_mode = int(os.environ.get("FOTO_CG_MODE", "2" if world == 1 else "0"))
     dist = None
     nccl_id = None
     if world > 1:

@@ -232,13 +232,9 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_HIP_CHECK(launch_init_mu(s.g, s.rho0, s.rhoT, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->s));
         if (c->o.cg_mode == 1 || c->o.cg_mode == 2) {
             s.spec.reset(new SpectralPlan());
-            FOTO_TRY(s.spec->init(s.g, W, c->r, c->eps, c->o.cg_mode, c->s));
+            FOTO_TRY(s.spec->init(s.g, s.rank, W, c->r, c->eps, c->o.cg_mode, c->s));
         }
         c->sh.push_back(std::move(sp));
-    }
-    if (c->o.cg_mode != 0 && W > 1) {
-        set_error("spectral CG (cg_mode=1) is single-shard only in this build");
-        return FOTO_ERR_ARG;
     }
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     return 0;
@@ -292,6 +288,95 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
     return 0;
 }
 
+// all-to-all between the physical slabs and the spectral row boxes (SpectralPlan):
+//   forward : rank g sends stage_g[nloc_g*Nx*y0_h, + nloc_g*nyl_h*Nx]  -> box_in_h[t0_g*nyl_h*Nx, ...]
+//   backward: rank g sends box_out_g[t0_h*nyl_g*Nx, + nloc_h*nyl_g*Nx] -> stage_h[nloc_h*Nx*y0_g, ...]
+static int alltoall_spec(foto_bb_ctx* c, bool forward) {
+    const int W = c->W;
+    const int64_t Nx = c->Nx;
+    auto slab = [&](int h, int* t0, int* nl) { split_planes(c->Nt, W, h, t0, nl); };
+    auto rows = [&](int h, int* y0, int* ny) { split_planes(c->Ny, W, h, y0, ny); };
+    // region rank a sends to rank b (and b receives from a), in doubles
+    auto region = [&](int a, int b, int64_t* soff, int64_t* roff, int64_t* cnt) {
+        int ta, na, tb, nb, ya, nya, yb, nyb;
+        slab(a, &ta, &na); slab(b, &tb, &nb); rows(a, &ya, &nya); rows(b, &yb, &nyb);
+        if (forward) {
+            *soff = (int64_t)na * Nx * yb; *cnt = (int64_t)na * nyb * Nx; *roff = (int64_t)ta * nyb * Nx;
+        } else {
+            *soff = (int64_t)tb * nya * Nx; *cnt = (int64_t)nb * nya * Nx; *roff = (int64_t)nb * Nx * ya;
+        }
+    };
+    auto sbuf = [&](Shard& s) { return forward ? s.spec->stage() : s.spec->box_out(); };
+    auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.spec->stage(); };
+    if (!c->rccl) {
+        for (auto& a : c->sh)
+            for (auto& b : c->sh) {
+                int64_t so, ro, n;
+                region(a->rank, b->rank, &so, &ro, &n);
+                if (n > 0)
+                    FOTO_HIP_CHECK(hipMemcpyAsync(rbuf(*b) + ro, sbuf(*a) + so, n * sizeof(double),
+                                                  hipMemcpyDeviceToDevice, c->s));
+            }
+        return 0;
+    }
+    Shard& s = *c->sh[0];
+    const int g = s.rank;
+    FOTO_NCCL_CHECK(ncclGroupStart());
+    for (int h = 0; h < W; ++h) {
+        if (h == g) continue;
+        int64_t so, ro, n;
+        region(g, h, &so, &ro, &n);   // what g sends to h
+        if (n > 0) FOTO_NCCL_CHECK(ncclSend(sbuf(s) + so, (size_t)n, ncclDouble, h, c->nc, c->s));
+        region(h, g, &so, &ro, &n);   // what g receives from h
+        if (n > 0) FOTO_NCCL_CHECK(ncclRecv(rbuf(s) + ro, (size_t)n, ncclDouble, h, c->nc, c->s));
+    }
+    FOTO_NCCL_CHECK(ncclGroupEnd());
+    int64_t so, ro, n;
+    region(g, g, &so, &ro, &n);
+    if (n > 0)
+        FOTO_HIP_CHECK(hipMemcpyAsync(rbuf(s) + ro, sbuf(s) + so, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+    return 0;
+}
+
+// Spectral s-step CG over time-slab shards: x/y DCTs on the own planes, all-to-all to
+// row boxes, t-DCT, pointwise CG passes with one 21-double all-gather each (moments summed
+// in rank order on every rank, so all ranks plan identically), then back.
+static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
+    const int maxiter = c->o.cg_maxiter;
+    const double rtol = c->o.cg_rtol;
+    const int M = SpectralPlan::moments();
+    KTimer* kt = &c->kt;
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_local(sp->rv, kt, c->s));
+    FOTO_TRY(alltoall_spec(c, true));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_t(kt, c->s));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_begin(rtol, maxiter, kt, c->s));
+    FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));
+    int passes = 0, done = 0, its = 0;
+    const int first = c->last_cg > 6 ? (c->last_cg - 4) / 2 : 4;
+    while (true) {
+        const int chunk = (passes == 0) ? first : 1;
+        for (int j = 0; j < chunk; ++j, ++passes) {
+            for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_pass(rtol, maxiter, kt, c->s));
+            FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
+            for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(0, rtol, maxiter, c->s));
+        }
+        FOTO_TRY(c->sh[0]->spec->poll(&done, &its, c->s));
+        if (done) break;
+        if (passes > maxiter + 4) {
+            set_error("sharded spectral CG did not terminate");
+            return FOTO_ERR_STATE;
+        }
+    }
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
+    FOTO_TRY(alltoall_spec(c, false));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
+    *iters = its;
+    *info = (done == 1) ? 0 : maxiter;
+    c->last_cg = its;
+    return 0;
+}
+
 // Solve A x = F (F already in rv, F.F gathered in gath_rr) to scipy's stopping rule.
 // The loop runs on the device; the host only polls the done flag between chunks.  Every
 // rank takes the same decisions (the flag is a function of gathered scalars), so the
@@ -299,6 +384,7 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
 static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
     const int maxiter = c->o.cg_maxiter;
     if (c->o.cg_mode != 0) {
+        if (c->W > 1) return cg_solve_spectral_sharded(c, iters, info);
         Shard& s = *c->sh[0];
         FOTO_TRY(s.spec->solve(s.rv, s.phi, c->o.cg_rtol, maxiter, c->last_cg, iters, info, &c->kt, c->s));
         c->last_cg = *iters;

@@ -4,13 +4,31 @@
 
 namespace foto {
 
-struct KTimer;
-
 struct SpectralPlan {
-    int init(const Geo& g, int world, double r, double eps, int sstep, hipStream_t s);
-    // b (physical, overwritten as scratch) -> x (physical); scipy stopping rule.
+    // rank / world: the shard's place in the time-slab decomposition (world > 1 needs
+    // sstep = 2; the spectral box of rank g is rows [y0, y0 + nyl) of every kt plane).
+    int init(const Geo& g, int rank, int world, double r, double eps, int sstep, hipStream_t s);
+    // single shard: b (physical, clobbered) -> x (physical); scipy stopping rule.
     int solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info, KTimer* kt,
               hipStream_t s);
+
+    // ---- sharded phases (driven by foto_bb.cpp, all-to-all / all-gather in between)
+    int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, pack -> stage
+    int fwd_t(KTimer* kt, hipStream_t s);                   // box_in (after all-to-all) -> b^
+    int cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s);   // r^ = b^, moments -> gath
+    int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // two CG steps, moments -> gath
+    int cg_plan(int init, double rtol, int maxiter, hipStream_t s);      // after the all-gather
+    int poll(int* done, int* iters, hipStream_t s);
+    int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
+    int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // unpack stage, inverse y, x
+    double* stage() const;     // physical-side all-to-all buffer [h][tl][rows of h][x]
+    double* box_in() const;    // box-side receive buffer [t][rows][x]
+    double* box_out() const;   // box-side send buffer of the inverse
+    double* gath() const;      // world * moments() doubles
+    static int moments();
+    int y0() const;
+    int nyl() const;
+
     ~SpectralPlan();
     void* impl = nullptr;
 };

@@ -195,12 +195,15 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 
 // ============================================================================ CG in the eigenbasis
 
+// The spectral box a shard owns: all kt, rows ky in [y0, y0 + nyl), all kx; laid out
+// [kt][ky - y0][kx] (single shard: the whole grid, y0 = 0, nyl = Ny).
 struct SpecTab {
     const double* mt;   // mu_t[kt]
     const double* my;   // mu_y[ky]
     const double* mx;   // mu_x[kx]
     double r, reps;     // r, r * eps
     int Nt, Ny, Nx;
+    int y0, nyl;
 };
 
 __device__ __forceinline__ double spec_lam(const SpecTab& T, double rowmu, int kx) {
@@ -212,7 +215,7 @@ __device__ __forceinline__ double spec_lam(const SpecTab& T, double rowmu, int k
 // i is even and both elements are 16-B aligned (one dwordx4 per lane).
 template <class F>
 __device__ __forceinline__ void spec_for_each(const SpecTab& T, F f) {
-    const int rows = T.Nt * T.Ny;
+    const int rows = T.Nt * T.nyl;
     const int ntx = (T.Nx + 127) / 128;
     const int ntiles = ntx * ((rows + 3) / 4);
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -220,7 +223,7 @@ __device__ __forceinline__ void spec_for_each(const SpecTab& T, F f) {
         const int row = (t / ntx) * 4 + ty;
         const int kx = (t % ntx) * 128 + 2 * tx;
         if (row >= rows || kx >= T.Nx) continue;
-        const int kt = row / T.Ny, ky = row - kt * T.Ny;
+        const int kt = row / T.nyl, ky = T.y0 + (row - kt * T.nyl);
         const double rowmu = T.mt[kt] + T.my[ky];
         const int64_t i = (int64_t)row * T.Nx + kx;
         const int n2 = (kx + 1 < T.Nx) ? 2 : 1;
@@ -444,10 +447,13 @@ __device__ __forceinline__ void cheb7(double x, double* T) {
     for (int m = 2; m < SM; ++m) T[m] = 2.0 * x * T[m - 1] - T[m - 2];
 }
 
+// gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
+// last block stores this shard's moments at gath[rank * 21]; after the all-gather,
+// k_spec_s2_plan sums them in rank order and plans (identically on every rank).
 template <bool VEC, bool INIT>
 __global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
                                                 const double* __restrict__ bh, SStep* Sg, RedBuf rb,
-                                                double rtol, int maxiter) {
+                                                double rtol, int maxiter, double* gath, int rank) {
     __shared__ SStep SS;
     if (threadIdx.x == 0) SS = *Sg;
     __syncthreads();
@@ -500,6 +506,10 @@ __global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ 
     });
     double tot[3 * SM];
     if (sp_reduce_last<3 * SM>(acc, rb, tot) && threadIdx.x == 0) {
+        if (gath) {
+            for (int m = 0; m < 3 * SM; ++m) gath[rank * 3 * SM + m] = tot[m];
+            return;
+        }
         SStep S = SS;
         if (INIT) {
             S.k = 0;
@@ -520,16 +530,81 @@ __global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ 
     }
 }
 
+// Multi-shard planning step (one thread): moments summed over ranks in rank order.
+__global__ void k_spec_s2_plan(SStep* Sg, const double* __restrict__ gath, int world, int init, double rtol,
+                               int maxiter) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    SStep S = *Sg;
+    double tot[3 * SM];
+    for (int m = 0; m < 3 * SM; ++m) tot[m] = 0.0;
+    for (int g = 0; g < world; ++g)
+        for (int m = 0; m < 3 * SM; ++m) tot[m] += gath[g * 3 * SM + m];
+    if (init) {
+        S.k = 0;
+        S.rho_prev = 0.0;
+        S.atol = fmax(0.0, rtol * sqrt(tot[0]));
+        S.done = 0;
+    } else {
+        if (S.done || S.nsteps == 0) return;   // the pass did nothing
+        S.k = S.k + S.nsteps;
+        if (S.fin) {
+            S.done = S.conv ? 1 : 2;
+            S.nsteps = 0;
+            *Sg = S;
+            return;
+        }
+    }
+    sstep2_plan(S, tot, tot + SM, tot + 2 * SM, maxiter);
+    *Sg = S;
+}
+
+// balanced contiguous split of n items over W parts (csrc/foto_bb.cpp split_planes)
+__device__ __forceinline__ int split_owner(int n, int W, int i) {
+    const int base = n / W, extra = n % W;
+    const int big = extra * (base + 1);
+    return (i < big) ? i / (base + 1) : extra + (i - big) / base;
+}
+__device__ __forceinline__ int split_start(int n, int W, int h) {
+    const int base = n / W, extra = n % W;
+    return h * base + (h < extra ? h : extra);
+}
+
+// own slab planes [tl][y][x] <-> all-to-all staging [h][tl][y - y0_h][x] (rows of peer h)
+template <bool PACK>
+__global__ __launch_bounds__(NT) void k_spec_pack(int nloc, int Ny, int Nx, int W, double* __restrict__ planes,
+                                                  double* __restrict__ stage) {
+    const int64_t n = (int64_t)nloc * Ny * Nx;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        const int64_t plane = (int64_t)Ny * Nx;
+        const int tl = (int)(i / plane);
+        const int64_t rem = i - tl * plane;
+        const int y = (int)(rem / Nx), x = (int)(rem - (int64_t)y * Nx);
+        const int h = split_owner(Ny, W, y);
+        const int y0h = split_start(Ny, W, h), nyh = split_start(Ny, W, h + 1) - y0h;
+        const int64_t j = (int64_t)nloc * Nx * y0h + ((int64_t)tl * nyh + (y - y0h)) * Nx + x;
+        if (PACK) stage[j] = planes[i];
+        else planes[i] = stage[j];
+    }
+}
+
 // ============================================================================ plan
+
+static int split_start_h(int n, int W, int h) {
+    const int base = n / W, extra = n % W;
+    return h * base + std::min(h, extra);
+}
 
 struct SpecImpl {
     Geo g{};
+    int rank = 0, world = 1;
+    int y0 = 0, nyl = 0;          // spectral box rows (sharded: Ny split over ranks)
     double r = 1, eps = 0;
-    double *bh = nullptr, *rh = nullptr, *ph = nullptr, *tmp = nullptr;
+    double *bh = nullptr, *rh = nullptr, *ph = nullptr, *tmp = nullptr;   // spectral box
+    double *tmpp = nullptr, *stage = nullptr;                               // physical slab scratch
     double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
     double *mx = nullptr, *my = nullptr, *mt = nullptr;
     RedBuf rb{};
-    double* gath = nullptr;
+    double* gath = nullptr;       // s = 1: 2 doubles; s = 2 sharded: world * 21
     CGScal* S = nullptr;
     CGScal* hS = nullptr;
     SStep* S2 = nullptr;
@@ -538,6 +613,7 @@ struct SpecImpl {
     int sstep = 1;
     std::vector<void*> allocs;
     int nblocks = 0;
+    double c0 = 0, c1 = 1;
 
     int alloc(size_t bytes, void** p) {
         FOTO_HIP_CHECK(hipMalloc(p, bytes));
@@ -553,8 +629,11 @@ struct SpecImpl {
         SpecTab T;
         T.mt = mt; T.my = my; T.mx = mx; T.r = r; T.reps = r * eps;
         T.Nt = g.Nt; T.Ny = g.Ny; T.Nx = g.Nx;
+        T.y0 = y0; T.nyl = nyl;
         return T;
     }
+    bool vec() const { return (g.Nx % 2) == 0; }
+    double nbox() const { return (double)g.Nt * nyl * g.Nx; }
 };
 
 // orthonormal DCT-II matrix C[k][j] = s_k cos(pi k (2j+1) / (2n)) (long double on the host)
@@ -574,13 +653,17 @@ static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, s
     }
 }
 
-int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep, hipStream_t s) {
+int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, int sstep, hipStream_t s) {
     if (sstep != 1 && sstep != 2) {
         set_error("spectral CG: s-step must be 1 or 2");
         return FOTO_ERR_ARG;
     }
-    if (world != 1 || g.nloc != g.Nt) {
-        set_error("spectral CG needs the whole time axis on one shard");
+    if (world > 1 && sstep != 2) {
+        set_error("sharded spectral CG needs cg_mode = 2 (s-step)");
+        return FOTO_ERR_ARG;
+    }
+    if (world > g.Ny) {
+        set_error("sharded spectral CG needs Ny >= world (rows are split over ranks)");
         return FOTO_ERR_ARG;
     }
     if (!(eps > 0.0)) {
@@ -591,14 +674,23 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep,
     impl = P;
     P->sstep = sstep;
     P->g = g;
+    P->rank = rank;
+    P->world = world;
+    P->y0 = split_start_h(g.Ny, world, rank);
+    P->nyl = split_start_h(g.Ny, world, rank + 1) - P->y0;
     P->r = r;
     P->eps = eps;
-    const size_t N = (size_t)g.Nt * g.nxy;
+    const size_t NB = (size_t)g.Nt * P->nyl * g.Nx;          // spectral box
+    const size_t NS = (size_t)g.nloc * g.nxy;                // physical slab
     void* b;
-    FOTO_TRY(P->alloc(N * 8, &b)); P->bh = (double*)b;
-    FOTO_TRY(P->alloc(N * 8, &b)); P->rh = (double*)b;
-    FOTO_TRY(P->alloc(N * 8, &b)); P->ph = (double*)b;
-    FOTO_TRY(P->alloc(N * 8, &b)); P->tmp = (double*)b;
+    FOTO_TRY(P->alloc(NB * 8, &b)); P->bh = (double*)b;
+    FOTO_TRY(P->alloc(NB * 8, &b)); P->rh = (double*)b;
+    FOTO_TRY(P->alloc(NB * 8, &b)); P->ph = (double*)b;
+    FOTO_TRY(P->alloc(std::max(NB, NS) * 8, &b)); P->tmp = (double*)b;
+    if (world > 1) {
+        FOTO_TRY(P->alloc(NS * 8, &b)); P->tmpp = (double*)b;
+        FOTO_TRY(P->alloc(NS * 8, &b)); P->stage = (double*)b;
+    }
     std::vector<double> C, CT, mu;
     auto up = [&](int n, double** Cd, double** CTd, double** mud) -> int {
         dct_matrix(n, C, CT, mu);
@@ -609,12 +701,19 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep,
         FOTO_HIP_CHECK(hipMemcpy(*Cd, C.data(), C.size() * 8, hipMemcpyHostToDevice));
         FOTO_HIP_CHECK(hipMemcpy(*CTd, CT.data(), CT.size() * 8, hipMemcpyHostToDevice));
         FOTO_HIP_CHECK(hipMemcpy(*mud, mu.data(), mu.size() * 8, hipMemcpyHostToDevice));
-        return 0;
+        return (int)0;
     };
     FOTO_TRY(up(g.Nx, &P->Cx, &P->CxT, &P->mx));
+    const double mx_max = mu.back();
     FOTO_TRY(up(g.Ny, &P->Cy, &P->CyT, &P->my));
+    const double my_max = mu.back();
     FOTO_TRY(up(g.Nt, &P->Ct, &P->CtT, &P->mt));
-    const int rows = g.Nt * g.Ny;
+    const double mt_max = mu.back();
+    // Chebyshev scaling of lam: global spectrum bounds (identical on every rank)
+    const double lmin = r * eps, lmax = r * eps + r * (mt_max + my_max + mx_max);
+    P->c0 = 0.5 * (lmax + lmin);
+    P->c1 = 0.5 * (lmax - lmin);
+    const int rows = g.Nt * P->nyl;
     const int ntiles = ((g.Nx + 127) / 128) * ((rows + 3) / 4);
     P->nblocks = std::min(ntiles, 2048);
     P->nblocks2 = std::min(ntiles, 512);
@@ -624,7 +723,7 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep,
     P->rb.ticket = (unsigned*)((double*)b + cap);
     P->rb.cap = cap;
     FOTO_HIP_CHECK(hipMemset(P->rb.ticket, 0, 8 * sizeof(double)));
-    FOTO_TRY(P->alloc(sizeof(double) * 4, &b)); P->gath = (double*)b;
+    FOTO_TRY(P->alloc(sizeof(double) * std::max(4, 3 * SM * world), &b)); P->gath = (double*)b;
     FOTO_TRY(P->alloc(sizeof(CGScal), &b)); P->S = (CGScal*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
     FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
@@ -635,7 +734,7 @@ int SpectralPlan::init(const Geo& g, int world, double r, double eps, int sstep,
 
 SpectralPlan::~SpectralPlan() { delete (SpecImpl*)impl; }
 
-// 3-D transforms: forward = (Ct (x) Cy (x) Cx), inverse = transpose.
+// 3-D transforms of a single shard: forward = (Ct (x) Cy (x) Cx), inverse = transpose.
 static int forward3(SpecImpl* P, double* in, double* scratch, double* out, KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
@@ -660,25 +759,35 @@ static int inverse3(SpecImpl* P, double* in, double* scratch, double* out, KTime
     return 0;
 }
 
-static int solve_s2(SpecImpl* P, const SpecTab& T, bool vec, double rtol, int maxiter, int predicted, int* iters,
-                    int* info, KTimer* kt, hipStream_t s) {
-    const Geo& g = P->g;
-    const double N = (double)g.Nt * (double)g.nxy;
+static hipError_t launch_s2(SpecImpl* P, bool init, double rtol, int maxiter, double* gath, hipStream_t s) {
+    const SpecTab T = P->tab();
+    if (P->vec()) {
+        if (init) k_spec_s2<true, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+        else k_spec_s2<true, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+    } else {
+        if (init) k_spec_s2<false, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+        else k_spec_s2<false, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+    }
+    return hipGetLastError();
+}
+
+static int reset_s2(SpecImpl* P, hipStream_t s) {
     SStep h{};
-    std::vector<double> mt(g.Nt), my(g.Ny), mx(g.Nx);
-    FOTO_HIP_CHECK(hipMemcpy(mt.data() + g.Nt - 1, P->mt + g.Nt - 1, 8, hipMemcpyDeviceToHost));
-    FOTO_HIP_CHECK(hipMemcpy(my.data() + g.Ny - 1, P->my + g.Ny - 1, 8, hipMemcpyDeviceToHost));
-    FOTO_HIP_CHECK(hipMemcpy(mx.data() + g.Nx - 1, P->mx + g.Nx - 1, 8, hipMemcpyDeviceToHost));
-    const double lmin = T.reps, lmax = T.reps + T.r * (mt[g.Nt - 1] + my[g.Ny - 1] + mx[g.Nx - 1]);
-    h.c0 = 0.5 * (lmax + lmin);
-    h.c1 = 0.5 * (lmax - lmin);
+    h.c0 = P->c0;
+    h.c1 = P->c1;
     *P->hS2 = h;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->S2, P->hS2, sizeof(SStep), hipMemcpyHostToDevice, s));
+    FOTO_HIP_CHECK(hipStreamSynchronize(s));   // hS2 is reused by polling
+    return 0;
+}
+
+static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* iters, int* info, KTimer* kt,
+                    hipStream_t s) {
+    const double N = P->nbox();
+    FOTO_TRY(reset_s2(P, s));
     {
         hipEvent_t e = kt ? kt->start(s) : nullptr;
-        if (vec) k_spec_s2<true, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
-        else k_spec_s2<false, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
-        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, nullptr, s));
         if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * N);
     }
     int passes = 0;
@@ -687,9 +796,7 @@ static int solve_s2(SpecImpl* P, const SpecTab& T, bool vec, double rtol, int ma
         const int chunk = (passes == 0) ? first : 1;
         for (int j = 0; j < chunk; ++j, ++passes) {
             hipEvent_t e = kt ? kt->start(s) : nullptr;
-            if (vec) k_spec_s2<true, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
-            else k_spec_s2<false, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter);
-            FOTO_HIP_CHECK(hipGetLastError());
+            FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, nullptr, s));
             if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * N);
         }
         FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
@@ -705,20 +812,25 @@ static int solve_s2(SpecImpl* P, const SpecTab& T, bool vec, double rtol, int ma
     return 0;
 }
 
+static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
+    const SpecTab T = P->tab();
+    if (P->vec()) k_spec_xhat<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+    else k_spec_xhat<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
+    return hipGetLastError();
+}
+
 int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info,
                         KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
     const SpecTab T = P->tab();
     const double N = (double)g.Nt * (double)g.nxy;
+    const bool vec = P->vec();
     // b (physical) -> b^ ; b is scratch afterwards
-    const bool vec = (g.Nx % 2) == 0;
     FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
     if (P->sstep == 2) {
-        FOTO_TRY(solve_s2(P, T, vec, rtol, maxiter, predicted, iters, info, kt, s));
-        if (vec) k_spec_xhat<true><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
-        else k_spec_xhat<false><<<P->nblocks, NT, 0, s>>>(T, P->bh, P->rh, P->tmp);
-        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_TRY(solve_s2(P, rtol, maxiter, predicted, iters, info, kt, s));
+        FOTO_HIP_CHECK(launch_xhat(P, s));
         FOTO_TRY(inverse3(P, P->tmp, b, x, kt, s));
         return 0;
     }
@@ -751,5 +863,96 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     FOTO_TRY(inverse3(P, P->tmp, b, x, kt, s));
     return 0;
 }
+
+// ----------------------------------------------------------------------------- sharded phases
+// Physical slab [tl][y][x] (planes t0..t0+nloc) <-> spectral box [kt][ky - y0][kx].
+
+int SpectralPlan::fwd_local(double* b, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    const Geo& g = P->g;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(dct_axis(g.nloc * g.Ny, g.Nx, 1, P->Cx, b, P->tmpp, s));      // x
+    FOTO_HIP_CHECK(dct_axis(g.nloc, g.Ny, g.Nx, P->Cy, P->tmpp, b, s));          // y
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    k_spec_pack<true><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world, b,
+                                                                                     P->stage);
+    FOTO_HIP_CHECK(hipGetLastError());
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
+    return 0;
+}
+
+int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    const Geo& g = P->g;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(dct_axis(1, g.Nt, P->nyl * g.Nx, P->Ct, P->tmp, P->bh, s));   // box tmp -> b^
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
+    return 0;
+}
+
+int SpectralPlan::cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    FOTO_TRY(reset_s2(P, s));
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, P->gath, s));
+    if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * P->nbox());
+    return 0;
+}
+
+int SpectralPlan::cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, P->gath, s));
+    if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * P->nbox());
+    return 0;
+}
+
+int SpectralPlan::cg_plan(int init, double rtol, int maxiter, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    k_spec_s2_plan<<<1, 64, 0, s>>>(P->S2, P->gath, P->world, init, rtol, maxiter);
+    FOTO_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int SpectralPlan::poll(int* done, int* iters, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
+    FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    *done = P->hS2->done;
+    *iters = P->hS2->iters;
+    return 0;
+}
+
+int SpectralPlan::inv_t(KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    const Geo& g = P->g;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(launch_xhat(P, s));                                              // tmp = x^
+    FOTO_HIP_CHECK(dct_axis(1, g.Nt, P->nyl * g.Nx, P->CtT, P->tmp, P->rh, s));    // rh = box of x~
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
+    return 0;
+}
+
+int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    const Geo& g = P->g;
+    const int64_t n = (int64_t)g.nloc * g.nxy;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    k_spec_pack<false><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world,
+                                                                                      scratch, P->stage);
+    FOTO_HIP_CHECK(hipGetLastError());
+    FOTO_HIP_CHECK(dct_axis(g.nloc, g.Ny, g.Nx, P->CyT, scratch, P->tmpp, s));     // y
+    FOTO_HIP_CHECK(dct_axis(g.nloc * g.Ny, g.Nx, 1, P->CxT, P->tmpp, x, s));       // x
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
+    return 0;
+}
+
+double* SpectralPlan::stage() const { return ((SpecImpl*)impl)->stage; }
+double* SpectralPlan::box_in() const { return ((SpecImpl*)impl)->tmp; }
+double* SpectralPlan::box_out() const { return ((SpecImpl*)impl)->rh; }
+double* SpectralPlan::gath() const { return ((SpecImpl*)impl)->gath; }
+int SpectralPlan::moments() { return 3 * SM; }
+int SpectralPlan::y0() const { return ((SpecImpl*)impl)->y0; }
+int SpectralPlan::nyl() const { return ((SpecImpl*)impl)->nyl; }
 
 }  // namespace foto

@@ -163,16 +163,19 @@ def test_bb_solve_c1(gold, mode):
         np.testing.assert_allclose(a, b, rtol=0, atol=1e-5)
 
 
-@pytest.mark.parametrize("vr", [2, 3])
-def test_bb_virtual_ranks_match_single(gold, vr):
-    """The time-sharded path (halo planes, per-rank partial sums, trajectory relay) on one
-    device with `vr` in-process shards reproduces the single-shard solve."""
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("vr", [2, 3, 5])
+def test_bb_virtual_ranks_match_single(gold, vr, mode):
+    """The time-sharded path on one device with `vr` in-process shards reproduces the
+    single-shard solve.  mode 0: halo planes, per-rank partial sums, trajectory relay;
+    mode 2: additionally the slab <-> row-box all-to-alls around the spectral CG and the
+    rank-ordered moment all-gather."""
     d = gold("bb_tex.npz")
     Nt, Ny, Nx = (int(s) for s in d["shape"])
     r, tol, eps, max_it = d["params"]
     res = []
     for v_ in (1, vr):
-        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, virtual_ranks=v_) as s:
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, virtual_ranks=v_, cg_mode=mode) as s:
             s.iterate(int(max_it), tol, True)
             res.append((np.array(s.crit), np.array(s.cg_its), s.phi(), s.flow()))
     (c1, k1, p1, f1), (c2, k2, p2, f2) = res
@@ -250,6 +253,24 @@ def test_full_size_spectral_matches_stencil():
         assert np.max(np.abs(k0 - k1)) <= 1
         np.testing.assert_allclose(c1, c0, rtol=1e-6)
         np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6 * np.abs(p0).max())
+
+
+def test_full_size_sharded_spectral_matches_single():
+    """Bench grid, 4 in-process shards of the spectral s-step CG vs one shard."""
+    from foto.synthetic import translating_gaussian
+    Nt, Ny, Nx = 32, 480, 640
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = []
+    for vr in (1, 4):
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2, virtual_ranks=vr) as s:
+            s.iterate(2, 0.0, False)
+            out.append((np.array(s.cg_its), np.array(s.crit), s.phi(), s.flow()))
+    (k0, c0, p0, f0), (k1, c1, p1, f1) = out
+    assert np.max(np.abs(k0 - k1)) <= 1
+    np.testing.assert_allclose(c1, c0, rtol=1e-7)
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6 * np.abs(p0).max())
+    for a, b in zip(f0, f1):
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)
 
 
 def test_full_size_cg_true_residual():
