@@ -179,12 +179,14 @@ def test_bb_virtual_ranks_match_single(gold, vr, mode):
             s.iterate(int(max_it), tol, True)
             res.append((np.array(s.crit), np.array(s.cg_its), s.phi(), s.flow()))
     (c1, k1, p1, f1), (c2, k2, p2, f2) = res
+    # per-rank partial sums change the reduction order: CG counts may move by one at the
+    # rtol boundary, which moves phi by O(rtol) (same bars as against the reference)
     assert len(c1) == len(c2)
     assert np.max(np.abs(k1 - k2)) <= 1
-    np.testing.assert_allclose(c2, c1, rtol=1e-9)
-    np.testing.assert_allclose(p2, p1, rtol=0, atol=1e-8 * np.abs(p1).max())
+    np.testing.assert_allclose(c2, c1, rtol=1e-6)
+    np.testing.assert_allclose(p2, p1, rtol=0, atol=1e-6 * np.abs(p1).max())
     for a, b in zip(f1, f2):
-        np.testing.assert_allclose(b, a, rtol=0, atol=1e-8)
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)
 
 
 def test_bb_solver_state_and_stats(gold):
