@@ -14,6 +14,7 @@
 // The per-axis DCTs are GEMMs (n x n matrix applied along an axis) on f64 MFMA
 // (v_mfma_f64_16x16x4_f64), 64x64x16 block tiles staged through LDS.
 #include <cmath>
+#include <cstdlib>
 #include <memory>
 
 #include "foto_spectral.h"
@@ -82,6 +83,65 @@ __device__ bool sp_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
         for (int k = 0; k < K; ++k) tot[k] = acc[k];
         __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    return true;
+}
+
+// Variant for NTH-thread blocks and many quantities: per-block sums are finished by K
+// threads of wave 0 in parallel, and the last block reduces each quantity with all its
+// threads (one load per thread per quantity, issued back to back) -- the cross-block
+// step costs one round trip instead of K * nb / NTH dependent loads.  Deterministic.
+template <int K, int NTH>
+__device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* shared, K */) {
+    constexpr int NW = NTH / 64;
+    static_assert(K <= 64, "K partial sums are finished by wave 0");
+    __shared__ double sh[K * NW];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nb = gridDim.x;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double x = sp_wave_sum(v[k]);
+        if (lane == 0) sh[k * NW + w] = x;
+    }
+    __syncthreads();
+    if (tid < K) {
+        double s = sh[tid * NW];
+#pragma unroll
+        for (int j = 1; j < NW; ++j) s += sh[tid * NW + j];
+        __hip_atomic_store(&rb.partials[(int64_t)tid * nb + blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (w == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // wave 0's stores drained before its ticket add
+        if (tid == 0) {
+            const unsigned t = __hip_atomic_fetch_add(rb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            is_last = (t == (unsigned)(nb - 1));
+        }
+    }
+    __syncthreads();
+    if (!is_last) return false;
+    double x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = 0.0;
+    for (int b = tid; b < nb; b += NTH) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            x[k] += __hip_atomic_load(&rb.partials[(int64_t)k * nb + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();   // sh reuse
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double y = sp_wave_sum(x[k]);
+        if (lane == 0) sh[k * NW + w] = y;
+    }
+    __syncthreads();
+    if (tid < K) {
+        double s = sh[tid * NW];
+#pragma unroll
+        for (int j = 1; j < NW; ++j) s += sh[tid * NW + j];
+        tot[tid] = s;
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
 
@@ -353,7 +413,9 @@ __global__ __launch_bounds__(NT) void k_spec_xhat(SpecTab T, const double* __res
 // inner products through the Gram matrix (M_{a+c} + M_{|a-c|}) / 2).  s = 2 reproduces
 // scipy's iterates to rounding (s >= 3 loses digits to the basis conditioning; measured).
 
-constexpr int SM = 7;   // moments 0..6 (polynomial degree <= 3 per factor)
+// Moments 0..3 suffice for s = 2: the inner products needed are p0.lam p0 (degree 1),
+// r1.r1 (degree 2) and p1.lam p1 (degree 3) in lam, and T_a T_b = (T_{a+b} + T_{|a-b|}) / 2.
+constexpr int SM = 4;
 
 struct SStep {
     int k;        // iterations applied so far
@@ -376,10 +438,12 @@ __device__ __forceinline__ double gram(const double* M, int a, int c) {
     return 0.5 * (M[a + c] + M[a > c ? a - c : c - a]);
 }
 
+// <U, V> over the measure; every product that occurs has total degree a + c <= 3 (the
+// coefficients above it are exactly zero), so only moments 0..3 are touched.
 __device__ double sp_ip(const SPoly& U, const SPoly& V, const double* Mrr, const double* Mrq, const double* Mqq) {
     double s = 0.0;
     for (int a = 0; a < 4; ++a)
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; a + c < SM; ++c) {
             s += U.r[a] * V.r[c] * gram(Mrr, a, c);
             s += U.r[a] * V.q[c] * gram(Mrq, a, c);
             s += U.q[a] * V.r[c] * gram(Mrq, c, a);
@@ -403,7 +467,7 @@ __device__ SPoly sp_mul_lam(const SPoly& U, double c0, double c1) {
 
 // next pass's scalars from the moments of (r_k, p_{k-1}); one thread.  scipy's loop:
 // top-of-iteration test ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p.
-__device__ void sstep2_plan(SStep& S, const double* Mrr, const double* Mrq, const double* Mqq, int maxiter) {
+__device__ __noinline__ void sstep2_plan(SStep& S, const double* Mrr, const double* Mrq, const double* Mqq, int maxiter) {
     SPoly R = {{1.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
     SPoly P = {{0.0, 0.0, 0.0, 0.0}, {1.0, 0.0, 0.0, 0.0}};
     double rho_prev = S.rho_prev;
@@ -440,7 +504,7 @@ __device__ void sstep2_plan(SStep& S, const double* Mrr, const double* Mrq, cons
     }
 }
 
-__device__ __forceinline__ void cheb7(double x, double* T) {
+__device__ __forceinline__ void cheb_all(double x, double* T) {
     T[0] = 1.0;
     T[1] = x;
 #pragma unroll
@@ -450,10 +514,48 @@ __device__ __forceinline__ void cheb7(double x, double* T) {
 // gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
 // last block stores this shard's moments at gath[rank * 21]; after the all-gather,
 // k_spec_s2_plan sums them in rank order and plans (identically on every rank).
-template <bool VEC, bool INIT>
-__global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
-                                                const double* __restrict__ bh, SStep* Sg, RedBuf rb,
-                                                double rtol, int maxiter, double* gath, int rank) {
+// element pair of tile t owned by this thread (see spec_for_each); n2 = 0: none
+struct SpElem {
+    int64_t i;
+    double l0, l1;
+    int n2;
+};
+
+template <int TR>
+__device__ __forceinline__ SpElem spec_elem(const SpecTab& T, int t, int ntx, int rows) {
+    SpElem e;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int row = (t / ntx) * TR + ty;
+    const int kx = (t % ntx) * 128 + 2 * tx;
+    e.n2 = 0;
+    e.i = 0;
+    e.l0 = e.l1 = 1.0;
+    if (row < rows && kx < T.Nx) {
+        const int kt = row / T.nyl, ky = T.y0 + (row - kt * T.nyl);
+        const double rowmu = T.mt[kt] + T.my[ky];
+        e.i = (int64_t)row * T.Nx + kx;
+        e.n2 = (kx + 1 < T.Nx) ? 2 : 1;
+        e.l0 = spec_lam(T, rowmu, kx);
+        e.l1 = (e.n2 == 2) ? spec_lam(T, rowmu, kx + 1) : 1.0;
+    }
+    return e;
+}
+
+// gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
+// last block stores this shard's moments at gath[rank * 21]; after the all-gather,
+// k_spec_s2_plan sums them in rank order and plans (identically on every rank).
+// The tile loop is software-pipelined: the next tile's r, q loads are issued before the
+// current tile is computed (two 16-B loads per lane in flight at all times).
+#ifndef FOTO_S2_NTH
+#define FOTO_S2_NTH 256
+#endif
+constexpr int S2_NTH = FOTO_S2_NTH;   // threads per block of the s-step pass
+
+template <bool VEC, bool INIT, bool FUSE>
+__global__ __launch_bounds__(S2_NTH) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
+                                                    const double* __restrict__ bh, SStep* Sg, RedBuf rb,
+                                                    double rtol, int maxiter, double* gath, int rank) {
+    constexpr int TR = S2_NTH / 64;   // tile = TR rows x 128 columns
     __shared__ SStep SS;
     if (threadIdx.x == 0) SS = *Sg;
     __syncthreads();
@@ -461,12 +563,14 @@ __global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ 
     const int k = SS.k, ns = SS.nsteps;
     const double a0 = SS.a[0], b0 = SS.b[0], a1 = SS.a[1], b1 = SS.b[1];
     const double c0 = SS.c0, ic1 = 1.0 / SS.c1;
+    const bool loadq = !INIT && k > 0;
+    const double* src = INIT ? bh : rh;
     double acc[3 * SM];
 #pragma unroll
     for (int m = 0; m < 3 * SM; ++m) acc[m] = 0.0;
     auto moments = [&](double lam, double r, double q) {
         double Tm[SM];
-        cheb7((lam - c0) * ic1, Tm);
+        cheb_all((lam - c0) * ic1, Tm);
         const double rr = r * r, rq = r * q, qq = q * q;
 #pragma unroll
         for (int m = 0; m < SM; ++m) {
@@ -475,38 +579,58 @@ __global__ __launch_bounds__(NT) void k_spec_s2(SpecTab T, double* __restrict__ 
             acc[2 * SM + m] += Tm[m] * qq;
         }
     };
-    spec_for_each(T, [&](int64_t i, double l0, double l1, int n2) {
-        double r0, r1, q0 = 0.0, q1 = 0.0;
-        if (INIT) {
-            ld2<VEC>(bh, i, n2, r0, r1);
-            st2<VEC>(rh, i, n2, r0, r1);
-        } else {
-            ld2<VEC>(rh, i, n2, r0, r1);
-            if (k > 0) ld2<VEC>(ph, i, n2, q0, q1);
-            // step 0 (iteration k)
-            double p0 = (k == 0) ? r0 : b0 * q0 + r0;
-            double p1 = (k == 0) ? r1 : b0 * q1 + r1;
-            r0 = r0 - a0 * (l0 * p0);
-            r1 = r1 - a0 * (l1 * p1);
-            q0 = p0;
-            q1 = p1;
-            if (ns == 2) {   // step 1 (iteration k + 1)
-                p0 = b1 * q0 + r0;
-                p1 = b1 * q1 + r1;
-                r0 = r0 - a1 * (l0 * p0);
-                r1 = r1 - a1 * (l1 * p1);
+    const int rows = T.Nt * T.nyl;
+    const int ntx = (T.Nx + 127) / 128;
+    const int ntiles = ntx * ((rows + TR - 1) / TR);
+    int t = blockIdx.x;
+    SpElem e = spec_elem<TR>(T, t < ntiles ? t : 0, ntx, rows);
+    if (t >= ntiles) e.n2 = 0;
+    double r0 = 0.0, r1 = 0.0, q0 = 0.0, q1 = 0.0;
+    if (e.n2) {
+        ld2<VEC>(src, e.i, e.n2, r0, r1);
+        if (loadq) ld2<VEC>(ph, e.i, e.n2, q0, q1);
+    }
+    while (t < ntiles) {
+        const int tn = t + gridDim.x;
+        SpElem en = spec_elem<TR>(T, tn < ntiles ? tn : 0, ntx, rows);
+        if (tn >= ntiles) en.n2 = 0;
+        double nr0 = 0.0, nr1 = 0.0, nq0 = 0.0, nq1 = 0.0;
+        if (en.n2) {
+            ld2<VEC>(src, en.i, en.n2, nr0, nr1);
+            if (loadq) ld2<VEC>(ph, en.i, en.n2, nq0, nq1);
+        }
+        if (e.n2) {
+            if (INIT) {
+                st2<VEC>(rh, e.i, e.n2, r0, r1);
+            } else {
+                // step 0 (iteration k): scipy's p = beta p + r; r -= alpha (A p)
+                double p0 = (k == 0) ? r0 : b0 * q0 + r0;
+                double p1 = (k == 0) ? r1 : b0 * q1 + r1;
+                r0 = r0 - a0 * (e.l0 * p0);
+                r1 = r1 - a0 * (e.l1 * p1);
                 q0 = p0;
                 q1 = p1;
+                if (ns == 2) {   // step 1 (iteration k + 1)
+                    p0 = b1 * q0 + r0;
+                    p1 = b1 * q1 + r1;
+                    r0 = r0 - a1 * (e.l0 * p0);
+                    r1 = r1 - a1 * (e.l1 * p1);
+                    q0 = p0;
+                    q1 = p1;
+                }
+                st2<VEC>(rh, e.i, e.n2, r0, r1);
+                st2<VEC>(ph, e.i, e.n2, q0, q1);
             }
-            st2<VEC>(rh, i, n2, r0, r1);
-            st2<VEC>(ph, i, n2, q0, q1);
+            moments(e.l0, r0, q0);
+            if (e.n2 == 2) moments(e.l1, r1, q1);
         }
-        moments(l0, r0, q0);
-        if (n2 == 2) moments(l1, r1, q1);
-    });
-    double tot[3 * SM];
-    if (sp_reduce_last<3 * SM>(acc, rb, tot) && threadIdx.x == 0) {
-        if (gath) {
+        e = en;
+        r0 = nr0; r1 = nr1; q0 = nq0; q1 = nq1;
+        t = tn;
+    }
+    __shared__ double tot[3 * SM];
+    if (sp_reduce_last_wide<3 * SM, S2_NTH>(acc, rb, tot) && threadIdx.x == 0) {
+        if (!FUSE) {
             for (int m = 0; m < 3 * SM; ++m) gath[rank * 3 * SM + m] = tot[m];
             return;
         }
@@ -611,6 +735,7 @@ struct SpecImpl {
     SStep* hS2 = nullptr;
     int nblocks2 = 0;
     int sstep = 1;
+    bool split_plan = false;
     std::vector<void*> allocs;
     int nblocks = 0;
     double c0 = 0, c1 = 1;
@@ -680,6 +805,10 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     P->nyl = split_start_h(g.Ny, world, rank + 1) - P->y0;
     P->r = r;
     P->eps = eps;
+    {
+        const char* e = getenv("FOTO_S2_SPLIT");   // tuning knob: plan in its own 1-block kernel
+        P->split_plan = e && atoi(e) != 0;
+    }
     const size_t NB = (size_t)g.Nt * P->nyl * g.Nx;          // spectral box
     const size_t NS = (size_t)g.nloc * g.nxy;                // physical slab
     void* b;
@@ -716,7 +845,11 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     const int rows = g.Nt * P->nyl;
     const int ntiles = ((g.Nx + 127) / 128) * ((rows + 3) / 4);
     P->nblocks = std::min(ntiles, 2048);
-    P->nblocks2 = std::min(ntiles, 512);
+    {
+        const int ntiles2 = ((g.Nx + 127) / 128) * ((rows + S2_NTH / 64 - 1) / (S2_NTH / 64));
+        const char* e = getenv("FOTO_S2_BLOCKS");   // tuning knob for A/B runs
+        P->nblocks2 = std::min(ntiles2, e ? std::max(1, atoi(e)) : 256 * 1024 / S2_NTH);
+    }
     const int cap = std::max(2 * P->nblocks, 3 * SM * P->nblocks2);
     FOTO_TRY(P->alloc(sizeof(double) * (cap + 8), &b));
     P->rb.partials = (double*)b;
@@ -761,13 +894,24 @@ static int inverse3(SpecImpl* P, double* in, double* scratch, double* out, KTime
 
 static hipError_t launch_s2(SpecImpl* P, bool init, double rtol, int maxiter, double* gath, hipStream_t s) {
     const SpecTab T = P->tab();
+    const int nb = P->nblocks2;
+    // gath == nullptr: single shard, fused plan (or the separate plan kernel, FOTO_S2_SPLIT=1)
+    const bool fuse = (gath == nullptr) && !P->split_plan;
+    double* gw = gath ? gath : P->gath;
+#define FOTO_S2_LAUNCH(V, I, F) \
+    k_spec_s2<V, I, F><<<nb, S2_NTH, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gw, P->rank)
     if (P->vec()) {
-        if (init) k_spec_s2<true, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
-        else k_spec_s2<true, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+        if (init) { if (fuse) FOTO_S2_LAUNCH(true, true, true); else FOTO_S2_LAUNCH(true, true, false); }
+        else { if (fuse) FOTO_S2_LAUNCH(true, false, true); else FOTO_S2_LAUNCH(true, false, false); }
     } else {
-        if (init) k_spec_s2<false, true><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
-        else k_spec_s2<false, false><<<P->nblocks2, NT, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gath, P->rank);
+        if (init) { if (fuse) FOTO_S2_LAUNCH(false, true, true); else FOTO_S2_LAUNCH(false, true, false); }
+        else { if (fuse) FOTO_S2_LAUNCH(false, false, true); else FOTO_S2_LAUNCH(false, false, false); }
     }
+#undef FOTO_S2_LAUNCH
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || gath != nullptr || fuse) return e;
+    // single shard, split plan: world = 1 plan kernel right behind the pass
+    k_spec_s2_plan<<<1, 64, 0, s>>>(P->S2, P->gath, 1, init ? 1 : 0, rtol, maxiter);
     return hipGetLastError();
 }
 
