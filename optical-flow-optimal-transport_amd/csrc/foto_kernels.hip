@@ -405,20 +405,38 @@ __global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mu
                                             const double* __restrict__ qx, const double* __restrict__ qy,
                                             const double* __restrict__ rho0, const double* __restrict__ rhoT,
                                             double r, double* __restrict__ F, RedBuf rb, double* gath, int rank) {
-    const int64_t n = (int64_t)g.nloc * g.nxy;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    // one thread per (x, y) column of a 64 x 4 tile, marching over the shard's planes; the
+    // t-field w_t = mu_t - r q_t of planes t-1, t, t+1 stays in registers (loaded one plane
+    // ahead), the x / y fields' neighbours are same-row / adjacent-row loads (L1 / L2 hits).
+    const int ntx = (g.Nx + TX - 1) / TX;
+    const int x = (blockIdx.x % ntx) * TX + (threadIdx.x & (TX - 1));
+    const int y = (blockIdx.x / ntx) * TY + threadIdx.x / TX;
+    const bool in = x < g.Nx && y < g.Ny;
+    const int64_t nxy = g.nxy, off = in ? (int64_t)y * g.Nx + x : 0;
+    const bool has_lo = g.t0 > 0, has_hi = g.t0 + g.nloc < g.Nt;
+    auto wt = [&](int l) { const int64_t i = l * nxy + off; return mut[i] - r * qt[i]; };
+    auto wx = [&](int64_t i) { return mux[i] - r * qx[i]; };
+    auto wy = [&](int64_t i) { return muy[i] - r * qy[i]; };
     double ff = 0.0;
-    if (i < n) {
-        const int l = (int)(i / g.nxy);
-        const int64_t off = i - (int64_t)l * g.nxy;
-        const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + l;
-        const double* M[3] = {mut, mux, muy};
-        const double* Q[3] = {qt, qx, qy};
-        double s = div_st_row(g, i, t, y, x, [&](int f, int64_t j) { return M[f][j] - r * Q[f][j]; });
-        if (t == 0) s -= (rho0[off] - mut[i]) + r * qt[i];
-        if (t == g.Nt - 1) s += (rhoT[off] - mut[i]) + r * qt[i];
-        F[i] = s;
-        ff = s * s;
+    if (in) {
+        double tm = has_lo ? wt(-1) : 0.0, tc = wt(0);
+        double tp = (g.nloc > 1 || has_hi) ? wt(1) : 0.0;
+        for (int l = 0; l < g.nloc; ++l) {
+            const int t = g.t0 + l;
+            const double tpp = (l + 2 < g.nloc || (l + 2 == g.nloc && has_hi)) ? wt(l + 2) : 0.0;
+            const int64_t i = l * nxy + off;
+            double s = 0.0;
+            acc_d1w(s, t, g.Nt, tm, tc, tp);
+            acc_d1w(s, x, g.Nx, x > 0 ? wx(i - 1) : 0.0, wx(i), x < g.Nx - 1 ? wx(i + 1) : 0.0);
+            acc_d1w(s, y, g.Ny, y > 0 ? wy(i - g.Nx) : 0.0, wy(i), y < g.Ny - 1 ? wy(i + g.Nx) : 0.0);
+            if (t == 0) s -= (rho0[off] - mut[i]) + r * qt[i];
+            if (t == g.Nt - 1) s += (rhoT[off] - mut[i]) + r * qt[i];
+            F[i] = s;
+            ff += s * s;
+            tm = tc;
+            tc = tp;
+            tp = tpp;
+        }
     }
     double v[1] = {ff}, tot[1];
     if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
@@ -427,8 +445,7 @@ __global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mu
 hipError_t launch_rhs(const Geo& g, const double* mut, const double* mux, const double* muy, const double* qt,
                       const double* qx, const double* qy, const double* rho0, const double* rhoT, double r,
                       double* F, RedBuf rb, double* gath, int rank, hipStream_t s) {
-    k_rhs<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb,
-                                                              gath, rank);
+    k_rhs<<<march_blocks(g), NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb, gath, rank);
     return hipGetLastError();
 }
 
@@ -458,8 +475,20 @@ hipError_t launch_init_mu(const Geo& g, const double* rho0, const double* rhoT, 
 
 // ============================================================================ stepB (A8)
 
-// Exact formulas and operation order of benamou_brenier.py:123-148 (glibc-pow constants
-// precomputed: (3/2)^(3/2) and the folded Python constants).
+// The projection of benamou_brenier.py:123-148 with the reference's branch tests and
+// closed forms, in an algebraically identical but cheaper form: (cos, sin)(atan2(b2, b1))
+// = (b1, b2) / |b|, x^(1/3) -> cbrt(x), (a+1)^3 and m^(3/2) by products.  Each changes a
+// result by at most an ulp or two (checked to 1e-12 against the reference's stepB in
+// tests/golden/stepb.npz, including both branches and the boundary); stepB runs once per
+// outer iteration on every voxel, and atan2 / cos / sin / pow would dominate it.
+// rare branch (a < -1, small |b|): kept out of line so its acos / cos do not inflate the
+// register allocation of the kernels that inline project_K
+__device__ __noinline__ double proj_trig_z(double al, double rho) {
+    const double m = -al - 1.0;
+    const double sm = sqrt(m);
+    return 1.632993161855452 * sm * cos(0.3333333333333333 * acos(1.8371173070873836 * rho / (m * sm)));
+}
+
 __device__ __forceinline__ void project_K(double al, double b1, double b2, double& oa, double& o1, double& o2) {
     if (2.0 * al + b1 * b1 + b2 * b2 <= 0.0) {
         oa = al; o1 = b1; o2 = b2;
@@ -467,27 +496,29 @@ __device__ __forceinline__ void project_K(double al, double b1, double b2, doubl
     }
     const double SQRT2 = 1.4142135623730951;
     const double rho = sqrt(b1 * b1 + b2 * b2);
-    const double th = atan2(b2, b1);
     const double ap1 = al + 1.0;
     double aH, rH;
-    if (-32.0 * pow(ap1, 3.0) - 108.0 * (rho * rho) < 0.0) {
+    if (-32.0 * (ap1 * ap1 * ap1) - 108.0 * (rho * rho) < 0.0) {
         const double S = 0.3535533905932738 * rho +
-                         0.16666666666666666 * sqrt(1.3333333333333333 * pow(al, 3.0) + 4.0 * (al * al) +
+                         0.16666666666666666 * sqrt(1.3333333333333333 * (al * al * al) + 4.0 * (al * al) +
                                                     4.5 * (rho * rho) + 4.0 * al + 1.3333333333333333);
-        const double c = pow(S, 0.3333333333333333);
+        const double c = cbrt(S);
         const double zh = (-0.3333333333333333 * ap1) / c + c;
         aH = -(zh * zh);
         rH = SQRT2 * zh;
     } else {
-        const double m = -al - 1.0;
-        const double zh = 1.632993161855452 * sqrt(m) *
-                          cos(0.3333333333333333 * acos(1.8371173070873836 * rho / pow(m, 1.5)));
+        const double zh = proj_trig_z(al, rho);
         aH = -0.5 * (zh * zh);
         rH = zh;
     }
     oa = aH;
-    o1 = rH * cos(th);
-    o2 = rH * sin(th);
+    if (rho > 0.0) {
+        o1 = rH * (b1 / rho);
+        o2 = rH * (b2 / rho);
+    } else {   // atan2(+-0, +0) = +-0, atan2(+-0, -0) = +-pi
+        o1 = signbit(b1) ? -rH : rH;
+        o2 = 0.0;
+    }
 }
 
 __global__ __launch_bounds__(NT) void k_stepB(int64_t M, const double* __restrict__ pa, const double* __restrict__ p1,
@@ -518,32 +549,32 @@ __global__ __launch_bounds__(NT) void k_prox(Geo g, const double* __restrict__ p
                                              double* __restrict__ qt, double* __restrict__ qx,
                                              double* __restrict__ qy, double r, double inv_r, RedBuf rb,
                                              double* gath, int rank) {
-    const int64_t n = (int64_t)g.nloc * g.nxy;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    // 2.5-D march over phi (64 x 4 LDS tile + halo, t-neighbours in registers), then the
+    // pointwise stepB / stepC / criterion terms of each voxel.
+    const int64_t nxy = g.nxy;
     double num = 0.0, den = 0.0;
-    if (i < n) {
-        const int l = (int)(i / g.nxy);
-        const int64_t off = i - (int64_t)l * g.nxy;
-        const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + l;
-        const double c = phi[i];
-        const double gt = d1w(t, g.Nt, t > 0 ? phi[i - g.nxy] : 0.0, c, t < g.Nt - 1 ? phi[i + g.nxy] : 0.0);
-        const double gx = d1w(x, g.Nx, x > 0 ? phi[i - 1] : 0.0, c, x < g.Nx - 1 ? phi[i + 1] : 0.0);
-        const double gy = d1w(y, g.Ny, y > 0 ? phi[i - g.Nx] : 0.0, c, y < g.Ny - 1 ? phi[i + g.Nx] : 0.0);
-        const double m0 = mut[i], m1 = mux[i], m2 = muy[i];
-        double a, b1, b2;
-        project_K(gt + inv_r * m0, gx + inv_r * m1, gy + inv_r * m2, a, b1, b2);
-        qt[i] = a;
-        qx[i] = b1;
-        qy[i] = b2;
-        double n0 = m0 + r * (gt - a);
-        n0 = (n0 < 0.0) ? 0.0 : n0;   // np.maximum(mu, 0) (NaN propagates)
-        mut[i] = n0;
-        mux[i] = m1 + r * (gx - b1);
-        muy[i] = m2 + r * (gy - b2);
-        const double gg = gx * gx + gy * gy;
-        num = n0 * fabs(gt + 0.5 * gg);
-        den = n0 * gg;
-    }
+    march(g, blockIdx.x, [&](int l, int64_t off) { return phi[l * nxy + off]; },
+          [&](int l, int t, int64_t off, int x, int y, double c, double xm, double xp, double ym, double yp,
+              double tm, double tp) {
+              const int64_t i = l * nxy + off;
+              const double gt = d1w(t, g.Nt, tm, c, tp);
+              const double gx = d1w(x, g.Nx, xm, c, xp);
+              const double gy = d1w(y, g.Ny, ym, c, yp);
+              const double m0 = mut[i], m1 = mux[i], m2 = muy[i];
+              double a, b1, b2;
+              project_K(gt + inv_r * m0, gx + inv_r * m1, gy + inv_r * m2, a, b1, b2);
+              qt[i] = a;
+              qx[i] = b1;
+              qy[i] = b2;
+              double n0 = m0 + r * (gt - a);
+              n0 = (n0 < 0.0) ? 0.0 : n0;   // np.maximum(mu, 0) (NaN propagates)
+              mut[i] = n0;
+              mux[i] = m1 + r * (gx - b1);
+              muy[i] = m2 + r * (gy - b2);
+              const double gg = gx * gx + gy * gy;
+              num += n0 * fabs(gt + 0.5 * gg);
+              den += n0 * gg;
+          });
     double v[2] = {num, den}, tot[2];
     if (grid_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) {
         gath[2 * rank] = tot[0];
@@ -553,8 +584,7 @@ __global__ __launch_bounds__(NT) void k_prox(Geo g, const double* __restrict__ p
 
 hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
                        double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s) {
-    k_prox<<<flat_blocks((int64_t)g.nloc * g.nxy), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, r, 1.0 / r, rb,
-                                                               gath, rank);
+    k_prox<<<march_blocks(g), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, r, 1.0 / r, rb, gath, rank);
     return hipGetLastError();
 }
 
