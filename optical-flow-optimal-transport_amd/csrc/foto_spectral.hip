@@ -241,14 +241,132 @@ __global__ __launch_bounds__(256) void k_dct_axis(int outer, int n, int inner, c
             }
 }
 
+// Large-tile variant: BM x BN = 128 x 128 per 256-thread block, each wave a 64 x 64
+// sub-tile (4 x 4 MFMA 16x16x4 accumulators), BK = 16.  The next K-step's A/B elements are
+// loaded into registers before the current step's MFMAs and written to the other LDS
+// buffer after them (one barrier per K-step): global latency overlaps the matrix work and
+// the loaded bytes per MFMA are half those of the 64 x 64 kernel.
+constexpr int LBM = 128, LBN = 128, LBK = 16;
+constexpr int LAS = LBK + 1;      // A row stride (doubles)
+constexpr int LBS = LBN + 16;     // B row stride: 144 doubles = 288 dwords = 32 mod 64
+
+template <bool CONTIG>
+__global__ __launch_bounds__(256) void k_dct_axis_l(int outer, int n, int inner, const double* __restrict__ M,
+                                                    const double* __restrict__ in, double* __restrict__ out) {
+    __shared__ double As[2][LBM * LAS];
+    __shared__ double Bs[2][LBK * LBS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int row0 = blockIdx.y * LBM, col0 = blockIdx.x * LBN;
+    const int nrows = CONTIG ? outer : n;
+    const int ncols = CONTIG ? n : inner;
+    const double* inb = CONTIG ? in : in + (int64_t)blockIdx.z * n * inner;
+    double* outb = CONTIG ? out : out + (int64_t)blockIdx.z * n * inner;
+
+    // staging map: 2048 A and 2048 B elements per K-step, 8 + 8 per thread
+    double ra[8], rb[8];
+    auto gload = [&](int j0) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            {   // A[m][kk], m = e / 16
+                const int m = e >> 4, kk = e & 15;
+                const int gr = row0 + m, gj = j0 + kk;
+                ra[q] = (gr < nrows && gj < n) ? (CONTIG ? inb[(int64_t)gr * n + gj] : M[(int64_t)gr * n + gj]) : 0.0;
+            }
+            if (CONTIG) {   // B[kk][c] = M[col0 + c][j0 + kk]
+                const int c = e >> 4, kk = e & 15;
+                const int gk = col0 + c, gj = j0 + kk;
+                rb[q] = (gk < ncols && gj < n) ? M[(int64_t)gk * n + gj] : 0.0;
+            } else {        // B[kk][c] = in[j0 + kk][col0 + c]
+                const int kk = e >> 7, c = e & 127;
+                const int gj = j0 + kk, gi = col0 + c;
+                rb[q] = (gj < n && gi < ncols) ? inb[(int64_t)gj * inner + gi] : 0.0;
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            As[buf][(e >> 4) * LAS + (e & 15)] = ra[q];
+            if (CONTIG) Bs[buf][(e & 15) * LBS + (e >> 4)] = rb[q];
+            else Bs[buf][(e >> 7) * LBS + (e & 127)] = rb[q];
+        }
+    };
+
+    dbl4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int j0 = 0; j0 < n; j0 += LBK) {
+        const bool more = j0 + LBK < n;
+        if (more) gload(j0 + LBK);
+#pragma unroll
+        for (int k4 = 0; k4 < LBK / 4; ++k4) {
+            const int kk = k4 * 4 + (lane >> 4);
+            double a[4], b[4];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) a[mi] = As[buf][(wm * 64 + mi * 16 + (lane & 15)) * LAS + kk];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[buf][kk * LBS + wn * 64 + ni * 16 + (lane & 15)];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gr = row0 + wm * 64 + mi * 16 + (lane >> 4) + 4 * r;
+                const int gc = col0 + wn * 64 + ni * 16 + (lane & 15);
+                if (gr < nrows && gc < ncols) {
+                    if (CONTIG) outb[(int64_t)gr * n + gc] = acc[mi][ni][r];
+                    else outb[(int64_t)gr * inner + gc] = acc[mi][ni][r];
+                }
+            }
+}
+
+static int g_dct_large = -1;   // FOTO_DCT_LARGE=0 selects the 64 x 64 kernel (A/B runs)
+
 static hipError_t dct_axis(int outer, int n, int inner, const double* M, const double* in, double* out,
                            hipStream_t s) {
+    if (g_dct_large < 0) {
+        const char* e = getenv("FOTO_DCT_LARGE");
+        g_dct_large = e ? atoi(e) : 1;
+    }
+    // the t-axis (n = Nt, small) keeps the 64 x 64 tile; x and y use 128 x 128
+    const bool large = g_dct_large && n >= 96;
     if (inner == 1) {
-        dim3 grid((n + BN - 1) / BN, (outer + BM - 1) / BM, 1);
-        k_dct_axis<true><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        if (large) {
+            dim3 grid((n + LBN - 1) / LBN, (outer + LBM - 1) / LBM, 1);
+            k_dct_axis_l<true><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        } else {
+            dim3 grid((n + BN - 1) / BN, (outer + BM - 1) / BM, 1);
+            k_dct_axis<true><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        }
     } else {
-        dim3 grid((inner + BN - 1) / BN, (n + BM - 1) / BM, outer);
-        k_dct_axis<false><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        if (large) {
+            dim3 grid((inner + LBN - 1) / LBN, (n + LBM - 1) / LBM, outer);
+            k_dct_axis_l<false><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        } else {
+            dim3 grid((inner + BN - 1) / BN, (n + BM - 1) / BM, outer);
+            k_dct_axis<false><<<grid, 256, 0, s>>>(outer, n, inner, M, in, out);
+        }
     }
     return hipGetLastError();
 }
