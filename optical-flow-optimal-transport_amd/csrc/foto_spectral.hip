@@ -86,31 +86,50 @@ __device__ bool sp_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
     return true;
 }
 
-// Variant for NTH-thread blocks and many quantities: per-block sums are finished by K
-// threads of wave 0 in parallel, and the last block reduces each quantity with all its
-// threads (one load per thread per quantity, issued back to back) -- the cross-block
-// step costs one round trip instead of K * nb / NTH dependent loads.  Deterministic.
+// Variant for NTH-thread blocks and many quantities (the s-step pass, K = 12).  Measured on
+// gfx950 (tools/s2_ablation.hip, 1024 blocks): the block sum is an LDS transpose (each
+// thread writes its K values, K x 16 threads sum 16-element segments, K threads the 16
+// segment sums) instead of K shuffle butterflies; partials are k-major ([k][block], so a
+// wave's load covers 4 cache lines); the last block issues all its loads before the first
+// use (clamped row index, unconditional) -- one round trip instead of one per load.
+// Fixed summation order: deterministic.
 template <int K, int NTH>
-__device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* shared, K */) {
-    constexpr int NW = NTH / 64;
-    static_assert(K <= 64, "K partial sums are finished by wave 0");
-    __shared__ double sh[K * NW];
-    __shared__ int is_last;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nb = gridDim.x;
+__device__ __forceinline__ void sp_blk_sum_lds(const double (&v)[K], double* red /* K*NTH */, double* red2 /* K*16 */) {
+    static_assert(NTH % 16 == 0 && K * 16 <= NTH, "segment layout");
+    const int tid = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double x = sp_wave_sum(v[k]);
-        if (lane == 0) sh[k * NW + w] = x;
+    for (int k = 0; k < K; ++k) red[k * NTH + tid] = v[k];
+    __syncthreads();
+    constexpr int SEG = NTH / 16;
+    if (tid < K * 16) {
+        const double* a = red + (tid >> 4) * NTH + (tid & 15) * SEG;
+        double s = a[0];
+#pragma unroll
+        for (int j = 1; j < SEG; ++j) s += a[j];
+        red2[tid] = s;
     }
     __syncthreads();
-    if (tid < K) {
-        double s = sh[tid * NW];
+}
+
+template <int K>
+__device__ __forceinline__ double sp_seg_total(const double* red2, int k) {
+    double s = red2[k * 16];
 #pragma unroll
-        for (int j = 1; j < NW; ++j) s += sh[tid * NW + j];
-        __hip_atomic_store(&rb.partials[(int64_t)tid * nb + blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (w == 0) {
+    for (int j = 1; j < 16; ++j) s += red2[k * 16 + j];
+    return s;
+}
+
+template <int K, int NTH>
+__device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* shared, K */) {
+    __shared__ double red[K * NTH];
+    __shared__ double red2[K * 16];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, nb = gridDim.x;
+    sp_blk_sum_lds<K, NTH>(v, red, red2);
+    if (tid < K)
+        __hip_atomic_store(&rb.partials[(int64_t)tid * nb + blockIdx.x], sp_seg_total<K>(red2, tid), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // wave 0's stores drained before its ticket add
         if (tid == 0) {
             const unsigned t = __hip_atomic_fetch_add(rb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -122,24 +141,26 @@ __device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* sh
     double x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = 0.0;
-    for (int b = tid; b < nb; b += NTH) {
+    constexpr int RPT = 4;   // blocks per thread per round trip
+    for (int base = 0; base < nb; base += RPT * NTH) {
+        double y[RPT][K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            x[k] += __hip_atomic_load(&rb.partials[(int64_t)k * nb + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();   // sh reuse
+        for (int j = 0; j < RPT; ++j) {
+            const int b = min(base + tid + j * NTH, nb - 1);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double y = sp_wave_sum(x[k]);
-        if (lane == 0) sh[k * NW + w] = y;
-    }
-    __syncthreads();
-    if (tid < K) {
-        double s = sh[tid * NW];
+            for (int k = 0; k < K; ++k)
+                y[j][k] = __hip_atomic_load(&rb.partials[(int64_t)k * nb + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
 #pragma unroll
-        for (int j = 1; j < NW; ++j) s += sh[tid * NW + j];
-        tot[tid] = s;
+        for (int j = 0; j < RPT; ++j) {
+            const bool ok = base + tid + j * NTH < nb;
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] += ok ? y[j][k] : 0.0;
+        }
     }
+    __syncthreads();   // red / red2 reuse
+    sp_blk_sum_lds<K, NTH>(x, red, red2);
+    if (tid < K) tot[tid] = sp_seg_total<K>(red2, tid);
     __syncthreads();
     if (tid == 0) __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
@@ -662,8 +683,8 @@ __device__ __forceinline__ SpElem spec_elem(const SpecTab& T, int t, int ntx, in
 // gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
 // last block stores this shard's moments at gath[rank * 21]; after the all-gather,
 // k_spec_s2_plan sums them in rank order and plans (identically on every rank).
-// The tile loop is software-pipelined: the next tile's r, q loads are issued before the
-// current tile is computed (two 16-B loads per lane in flight at all times).
+// A plain grid-stride tile loop: software-pipelining it (next tile's loads issued first)
+// measured 1 us slower -- the lam-table loads' waits drain the prefetch anyway.
 #ifndef FOTO_S2_NTH
 #define FOTO_S2_NTH 256
 #endif
@@ -700,51 +721,35 @@ __global__ __launch_bounds__(S2_NTH) void k_spec_s2(SpecTab T, double* __restric
     const int rows = T.Nt * T.nyl;
     const int ntx = (T.Nx + 127) / 128;
     const int ntiles = ntx * ((rows + TR - 1) / TR);
-    int t = blockIdx.x;
-    SpElem e = spec_elem<TR>(T, t < ntiles ? t : 0, ntx, rows);
-    if (t >= ntiles) e.n2 = 0;
-    double r0 = 0.0, r1 = 0.0, q0 = 0.0, q1 = 0.0;
-    if (e.n2) {
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const SpElem e = spec_elem<TR>(T, t, ntx, rows);
+        if (!e.n2) continue;
+        double r0, r1, q0 = 0.0, q1 = 0.0;
         ld2<VEC>(src, e.i, e.n2, r0, r1);
         if (loadq) ld2<VEC>(ph, e.i, e.n2, q0, q1);
-    }
-    while (t < ntiles) {
-        const int tn = t + gridDim.x;
-        SpElem en = spec_elem<TR>(T, tn < ntiles ? tn : 0, ntx, rows);
-        if (tn >= ntiles) en.n2 = 0;
-        double nr0 = 0.0, nr1 = 0.0, nq0 = 0.0, nq1 = 0.0;
-        if (en.n2) {
-            ld2<VEC>(src, en.i, en.n2, nr0, nr1);
-            if (loadq) ld2<VEC>(ph, en.i, en.n2, nq0, nq1);
-        }
-        if (e.n2) {
-            if (INIT) {
-                st2<VEC>(rh, e.i, e.n2, r0, r1);
-            } else {
-                // step 0 (iteration k): scipy's p = beta p + r; r -= alpha (A p)
-                double p0 = (k == 0) ? r0 : b0 * q0 + r0;
-                double p1 = (k == 0) ? r1 : b0 * q1 + r1;
-                r0 = r0 - a0 * (e.l0 * p0);
-                r1 = r1 - a0 * (e.l1 * p1);
+        if (INIT) {
+            st2<VEC>(rh, e.i, e.n2, r0, r1);
+        } else {
+            // step 0 (iteration k): scipy's p = beta p + r; r -= alpha (A p)
+            double p0 = (k == 0) ? r0 : b0 * q0 + r0;
+            double p1 = (k == 0) ? r1 : b0 * q1 + r1;
+            r0 = r0 - a0 * (e.l0 * p0);
+            r1 = r1 - a0 * (e.l1 * p1);
+            q0 = p0;
+            q1 = p1;
+            if (ns == 2) {   // step 1 (iteration k + 1)
+                p0 = b1 * q0 + r0;
+                p1 = b1 * q1 + r1;
+                r0 = r0 - a1 * (e.l0 * p0);
+                r1 = r1 - a1 * (e.l1 * p1);
                 q0 = p0;
                 q1 = p1;
-                if (ns == 2) {   // step 1 (iteration k + 1)
-                    p0 = b1 * q0 + r0;
-                    p1 = b1 * q1 + r1;
-                    r0 = r0 - a1 * (e.l0 * p0);
-                    r1 = r1 - a1 * (e.l1 * p1);
-                    q0 = p0;
-                    q1 = p1;
-                }
-                st2<VEC>(rh, e.i, e.n2, r0, r1);
-                st2<VEC>(ph, e.i, e.n2, q0, q1);
             }
-            moments(e.l0, r0, q0);
-            if (e.n2 == 2) moments(e.l1, r1, q1);
+            st2<VEC>(rh, e.i, e.n2, r0, r1);
+            st2<VEC>(ph, e.i, e.n2, q0, q1);
         }
-        e = en;
-        r0 = nr0; r1 = nr1; q0 = nq0; q1 = nq1;
-        t = tn;
+        moments(e.l0, r0, q0);
+        if (e.n2 == 2) moments(e.l1, r1, q1);
     }
     __shared__ double tot[3 * SM];
     if (sp_reduce_last_wide<3 * SM, S2_NTH>(acc, rb, tot) && threadIdx.x == 0) {
