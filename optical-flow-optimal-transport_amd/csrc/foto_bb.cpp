@@ -109,6 +109,7 @@ struct foto_bb_ctx {
     CGScal* hS = nullptr;                     // pinned host mirror of shard 0's CG scalars
     double* hgath = nullptr;                  // pinned host mirror of gath
     int last_cg = 0;
+    int last_passes = 0;   // s-step passes of the previous sharded spectral solve
     int have_phi = 0;
     // bookkeeping
     double prev_crit = -1;
@@ -339,7 +340,7 @@ static int alltoall_spec(foto_bb_ctx* c, bool forward) {
 }
 
 // Spectral s-step CG over time-slab shards: x/y DCTs on the own planes, all-to-all to
-// row boxes, t-DCT, pointwise CG passes with one 21-double all-gather each (moments summed
+// row boxes, t-DCT, pointwise CG passes with one NACC-double all-gather each (moments summed
 // in rank order on every rank, so all ranks plan identically), then back.
 static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     const int maxiter = c->o.cg_maxiter;
@@ -352,8 +353,8 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_begin(rtol, maxiter, kt, c->s));
     FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));
-    int passes = 0, done = 0, its = 0;
-    const int first = c->last_cg > 6 ? (c->last_cg - 4) / 2 : 4;
+    int passes = 0, done = 0, its = 0, planned = 0;
+    const int first = c->last_passes > 2 ? c->last_passes - 1 : 4;
     while (true) {
         const int chunk = (passes == 0) ? first : 1;
         for (int j = 0; j < chunk; ++j, ++passes) {
@@ -361,7 +362,7 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
             FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
             for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(0, rtol, maxiter, c->s));
         }
-        FOTO_TRY(c->sh[0]->spec->poll(&done, &its, c->s));
+        FOTO_TRY(c->sh[0]->spec->poll(&done, &its, &planned, c->s));
         if (done) break;
         if (passes > maxiter + 4) {
             set_error("sharded spectral CG did not terminate");
@@ -374,6 +375,7 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     *iters = its;
     *info = (done == 1) ? 0 : maxiter;
     c->last_cg = its;
+    c->last_passes = planned;
     return 0;
 }
 

@@ -16,9 +16,9 @@ struct SpectralPlan {
     int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, pack -> stage
     int fwd_t(KTimer* kt, hipStream_t s);                   // box_in (after all-to-all) -> b^
     int cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s);   // r^ = b^, moments -> gath
-    int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // two CG steps, moments -> gath
+    int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // planned CG steps, moments -> gath
     int cg_plan(int init, double rtol, int maxiter, hipStream_t s);      // after the all-gather
-    int poll(int* done, int* iters, hipStream_t s);
+    int poll(int* done, int* iters, int* passes, hipStream_t s);
     int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
     int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // unpack stage, inverse y, x
     double* stage() const;     // physical-side all-to-all buffer [h][tl][rows of h][x]

@@ -86,49 +86,78 @@ __device__ bool sp_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
     return true;
 }
 
-// Variant for NTH-thread blocks and many quantities (the s-step pass, K = 12).  Measured on
+// Variant for NTH-thread blocks and many quantities (the s-step pass, K = 48).  Measured on
 // gfx950 (tools/s2_ablation.hip, 1024 blocks): the block sum is an LDS transpose (each
-// thread writes its K values, K x 16 threads sum 16-element segments, K threads the 16
-// segment sums) instead of K shuffle butterflies; partials are k-major ([k][block], so a
-// wave's load covers 4 cache lines); the last block issues all its loads before the first
-// use (clamped row index, unconditional) -- one round trip instead of one per load.
-// Fixed summation order: deterministic.
-template <int K, int NTH>
-__device__ __forceinline__ void sp_blk_sum_lds(const double (&v)[K], double* red /* K*NTH */, double* red2 /* K*16 */) {
-    static_assert(NTH % 16 == 0 && K * 16 <= NTH, "segment layout");
+// thread writes CH of its values, CH x 16 threads sum 16-element segments, CH threads the
+// 16 segment sums), CH = 16 quantities at a time, instead of K shuffle butterflies;
+// partials are k-major ([k][block], so a wave's load covers 4 cache lines); the last block
+// issues a chunk's loads before the first use (clamped block index, unconditional) -- one
+// round trip per chunk instead of one per load.  Fixed summation order: deterministic.
+// Compensated (TwoSum) accumulation: s + c carries the running sum to ~2^-100 relative,
+// so the block sums are correctly rounded to within ~1 ulp.  The s-step plan's Gram-form
+// inner products cancel by up to S_CLIM and need moments that accurate: with plain fp64
+// trees the textured golden solve drifts to 1e-7 relative in crit, with compensated block
+// sums to 1e-8 (prototype measurement; tests/test_sstep_plan.py).
+__device__ __forceinline__ void two_sum_acc(double& s, double& c, double x) {
+    const double t = s + x;
+    const double bp = t - s;
+    c += (s - (t - bp)) + (x - bp);
+    s = t;
+}
+
+template <int CH, int NTH>
+__device__ __forceinline__ void sp_blk_sum_lds(const double* v /* CH values of this thread */, double* red /* CH*NTH */,
+                                               double* red2 /* 2*CH*16: sums | compensations */) {
+    static_assert(NTH % 16 == 0 && CH * 16 <= NTH, "segment layout");
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < K; ++k) red[k * NTH + tid] = v[k];
+    for (int k = 0; k < CH; ++k) red[k * NTH + tid] = v[k];
     __syncthreads();
     constexpr int SEG = NTH / 16;
-    if (tid < K * 16) {
+    if (tid < CH * 16) {
         const double* a = red + (tid >> 4) * NTH + (tid & 15) * SEG;
-        double s = a[0];
+        double s = a[0], c = 0.0;
 #pragma unroll
-        for (int j = 1; j < SEG; ++j) s += a[j];
+        for (int j = 1; j < SEG; ++j) two_sum_acc(s, c, a[j]);
         red2[tid] = s;
+        red2[CH * 16 + tid] = c;
     }
     __syncthreads();
 }
 
-template <int K>
+// total of quantity k's 16 compensated segment sums, rounded once
+template <int CH>
 __device__ __forceinline__ double sp_seg_total(const double* red2, int k) {
-    double s = red2[k * 16];
+    double s = red2[k * 16], c = red2[CH * 16 + k * 16];
 #pragma unroll
-    for (int j = 1; j < 16; ++j) s += red2[k * 16 + j];
-    return s;
+    for (int j = 1; j < 16; ++j) {
+        two_sum_acc(s, c, red2[k * 16 + j]);
+        c += red2[CH * 16 + k * 16 + j];
+    }
+    return s + c;
+}
+
+constexpr int sp_chunk(int K) {   // largest divisor of K that is <= 16
+    int c = K < 16 ? K : 16;
+    while (K % c) --c;
+    return c;
 }
 
 template <int K, int NTH>
 __device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* shared, K */) {
-    __shared__ double red[K * NTH];
-    __shared__ double red2[K * 16];
+    constexpr int CH = sp_chunk(K);
+    static_assert(K % CH == 0, "whole chunks");
+    __shared__ double red[CH * NTH];
+    __shared__ double red2[2 * CH * 16];
     __shared__ int is_last;
     const int tid = threadIdx.x, nb = gridDim.x;
-    sp_blk_sum_lds<K, NTH>(v, red, red2);
-    if (tid < K)
-        __hip_atomic_store(&rb.partials[(int64_t)tid * nb + blockIdx.x], sp_seg_total<K>(red2, tid), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int c = 0; c < K; c += CH) {
+        sp_blk_sum_lds<CH, NTH>(v + c, red, red2);
+        if (tid < CH)
+            __hip_atomic_store(&rb.partials[(int64_t)(c + tid) * nb + blockIdx.x], sp_seg_total<CH>(red2, tid),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (tid < 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // wave 0's stores drained before its ticket add
         if (tid == 0) {
@@ -138,29 +167,33 @@ __device__ bool sp_reduce_last_wide(double (&v)[K], RedBuf rb, double* tot /* sh
     }
     __syncthreads();
     if (!is_last) return false;
-    double x[K];
+    constexpr int RPT = 2;   // blocks per thread per round trip (register peak of the pass)
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = 0.0;
-    constexpr int RPT = 4;   // blocks per thread per round trip
-    for (int base = 0; base < nb; base += RPT * NTH) {
-        double y[RPT][K];
+    for (int c = 0; c < K; c += CH) {
+        double x[CH];
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) {
-            const int b = min(base + tid + j * NTH, nb - 1);
+        for (int k = 0; k < CH; ++k) x[k] = 0.0;
+        for (int base = 0; base < nb; base += RPT * NTH) {
+            double y[RPT][CH];
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                y[j][k] = __hip_atomic_load(&rb.partials[(int64_t)k * nb + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = 0; j < RPT; ++j) {
+                const int b = min(base + tid + j * NTH, nb - 1);
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    y[j][k] = __hip_atomic_load(&rb.partials[(int64_t)(c + k) * nb + b], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+                const bool ok = base + tid + j * NTH < nb;
+#pragma unroll
+                for (int k = 0; k < CH; ++k) x[k] += ok ? y[j][k] : 0.0;
+            }
         }
-#pragma unroll
-        for (int j = 0; j < RPT; ++j) {
-            const bool ok = base + tid + j * NTH < nb;
-#pragma unroll
-            for (int k = 0; k < K; ++k) x[k] += ok ? y[j][k] : 0.0;
-        }
+        __syncthreads();   // red / red2 reuse
+        sp_blk_sum_lds<CH, NTH>(x, red, red2);
+        if (tid < CH) tot[c + tid] = sp_seg_total<CH>(red2, tid);
     }
-    __syncthreads();   // red / red2 reuse
-    sp_blk_sum_lds<K, NTH>(x, red, red2);
-    if (tid < K) tot[tid] = sp_seg_total<K>(red2, tid);
     __syncthreads();
     if (tid == 0) __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
@@ -539,101 +572,183 @@ __global__ __launch_bounds__(NT) void k_spec_xhat(SpecTab T, const double* __res
     });
 }
 
-// ============================================================================ s-step (s = 2) CG in the eigenbasis
+// ============================================================================ s-step CG in the eigenbasis
 //
-// One pass = two CG iterations.  State between passes: r = r_k, q = p_{k-1}.  The pass
-// applies the two steps pointwise (p = beta q + r; r -= alpha lam p; q = p -- exactly
+// One pass = up to SMAX CG iterations.  State between passes: r = r_k, q = p_{k-1}.  The
+// pass applies the planned steps pointwise (p = beta q + r; r -= alpha lam p; q = p --
 // scipy's per-element recurrence) with scalars prepared by the previous pass, then
 // accumulates the Chebyshev moments of the NEW state,
 //     M^rr_m = sum T_m(x) r^2,  M^rq_m = sum T_m(x) r q,  M^qq_m = sum T_m(x) q^2,
-//     x = (lam - c0) / c1 in [-1, 1],  m = 0..6,
-// from which the last block computes the next two iterations' rho, p.Ap, alpha, beta and
-// the stop test (r_{k+i} = A_i(lam) r + B_i(lam) q with Chebyshev-coefficient polynomials;
-// inner products through the Gram matrix (M_{a+c} + M_{|a-c|}) / 2).  s = 2 reproduces
-// scipy's iterates to rounding (s >= 3 loses digits to the basis conditioning; measured).
+//     x = (lam - c0) / c1 in [-1, 1],  m = 0 .. 2 SMAX - 1,
+// from which one wavefront of the last block plans the next pass: r_{k+i} = A_i(lam) r +
+// B_i(lam) q with Chebyshev-coefficient polynomials, inner products through the Gram matrix
+// (M_{a+c} + M_{|a-c|}) / 2.  Step i > 0 is taken only while its two Gram-form inner
+// products (rho_{k+i} and p.Ap) are well conditioned: sum |terms| / |result| <= S_CLIM
+// (1e4, i.e. ~1e-12 relative rounding).  Early in a solve the residual measure is a few
+// dominant low-frequency components, the Chebyshev-Krylov basis is nearly degenerate and
+// passes take 1-2 steps; later ones take SMAX.  A fixed s >= 3 loses digits in the first
+// passes (measured: alpha off by 1e-4 at s = 3, k = 0).  tests/test_sstep_plan.py checks
+// the planning rule (numpy restatement) against the golden solves: the same CG counts as
+// scipy; at 640x480x32, 24 passes for 147 iterations (s = 2: 74).
 
-// Moments 0..3 suffice for s = 2: the inner products needed are p0.lam p0 (degree 1),
-// r1.r1 (degree 2) and p1.lam p1 (degree 3) in lam, and T_a T_b = (T_{a+b} + T_{|a-b|}) / 2.
-constexpr int SM = 4;
+#ifndef FOTO_SMAX
+#define FOTO_SMAX 8
+#endif
+constexpr int SMAX = FOTO_SMAX;      // max CG steps per pass
+constexpr int NMOM = 2 * SMAX;       // moments per family: degrees 0 .. 2 SMAX - 1
+constexpr int NACC = 3 * NMOM;       // rr, rq, qq
+constexpr int NCO = SMAX + 1;        // Chebyshev coefficients per part (degree <= SMAX)
+constexpr int NG = 2 * NCO;          // combined (r part, q part) coefficient index
+constexpr double S_CLIM = 1e4;       // cancellation limit of a Gram-form inner product
+static_assert(NG <= 64, "coefficients live one per lane");
 
 struct SStep {
     int k;        // iterations applied so far
-    int nsteps;   // steps the next pass applies (0, 1, 2)
+    int nsteps;   // steps the next pass applies (0 .. SMAX)
     int fin;      // after applying nsteps the solve is finished
     int conv;     // ... because the stop test passed (else: maxiter reached)
     int done;     // 1 converged, 2 maxiter reached (host polls this)
     int iters;    // iterations at finish
-    double a[2], b[2];
+    int passes;   // plans made in this solve
+    int pad;
+    double a[SMAX], b[SMAX];
     double rho_prev;   // rho_{k-1}
     double atol;
     double c0, c1;
 };
 
-struct SPoly {   // (coefficients on T_a(x) r, coefficients on T_a(x) q), a = 0..3
-    double r[4], q[4];
-};
+// Plan helpers.  Coefficient vectors are distributed one entry per lane: lane j < NG holds
+// index j of (r part | q part), lanes >= NG hold 0; lane j also holds row j of the Gram
+// matrix H.  Cross-lane traffic goes through the planning wave's LDS buffer xb (one
+// ds_write per lane, broadcast reads); one wave, so ordering only needs the
+// write-completion wait.
+#define FOTO_LDS_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-__device__ __forceinline__ double gram(const double* M, int a, int c) {
-    return 0.5 * (M[a + c] + M[a > c ? a - c : c - a]);
-}
-
-// <U, V> over the measure; every product that occurs has total degree a + c <= 3 (the
-// coefficients above it are exactly zero), so only moments 0..3 are touched.
-__device__ double sp_ip(const SPoly& U, const SPoly& V, const double* Mrr, const double* Mrq, const double* Mqq) {
-    double s = 0.0;
-    for (int a = 0; a < 4; ++a)
-        for (int c = 0; a + c < SM; ++c) {
-            s += U.r[a] * V.r[c] * gram(Mrr, a, c);
-            s += U.r[a] * V.q[c] * gram(Mrq, a, c);
-            s += U.q[a] * V.r[c] * gram(Mrq, c, a);
-            s += U.q[a] * V.q[c] * gram(Mqq, a, c);
+// <U, V> = sum_j U_j (H V)_j and its cancellation ratio sum |terms| / |<U, V>|; lanes 0 and
+// 1 sum the NG lane values (value, |terms|) in lane order, every lane reads the result.
+__device__ __forceinline__ double plan_ip(double U, double V, const double (&hrow)[NG], double* xb, double* cratio) {
+    const int lane = threadIdx.x & 63;
+    if (lane < NG) xb[lane] = V;
+    FOTO_LDS_WAIT();
+    double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < NG; c += 2) {
+        const double t0 = hrow[c] * xb[c];
+        const double t1 = (c + 1 < NG) ? hrow[c + 1] * xb[c + 1] : 0.0;
+        w0 += t0;
+        w1 += t1;
+        a0 += fabs(t0);
+        a1 += fabs(t1);
+    }
+    FOTO_LDS_WAIT();
+    if (lane < NG) {
+        xb[NG + lane] = U * (w0 + w1);
+        xb[2 * NG + lane] = fabs(U) * (a0 + a1);
+    }
+    FOTO_LDS_WAIT();
+    if (lane < 2) {
+        const double* src = xb + NG + lane * NG;
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NG; j += 2) {
+            s0 += src[j];
+            if (j + 1 < NG) s1 += src[j + 1];
         }
+        FOTO_LDS_WAIT();
+        xb[3 * NG + lane] = s0 + s1;
+    }
+    FOTO_LDS_WAIT();
+    const double s = xb[3 * NG], sa = xb[3 * NG + 1];
+    FOTO_LDS_WAIT();
+    *cratio = (s != 0.0) ? sa / fabs(s) : INFINITY;
     return s;
 }
 
-__device__ SPoly sp_mul_lam(const SPoly& U, double c0, double c1) {
-    SPoly Y;
-    auto one = [&](const double* c, double* y) {
-        double xc[4] = {0.0, 0.0, 0.0, 0.0};
-        xc[1] += c[0];
-        for (int m = 1; m < 3; ++m) { xc[m + 1] += 0.5 * c[m]; xc[m - 1] += 0.5 * c[m]; }
-        for (int m = 0; m < 4; ++m) y[m] = c0 * c[m] + c1 * xc[m];
-    };
-    one(U.r, Y.r);
-    one(U.q, Y.q);
-    return Y;
+// lam U = c0 U + c1 x U, x T_0 = T_1, x T_m = (T_{m+1} + T_{m-1}) / 2 within each part; the
+// top coefficient is never multiplied (its degree would exceed SMAX; it is zero whenever
+// this is called).
+__device__ __forceinline__ double plan_mul_lam(double U, double c0, double c1, double* xb) {
+    const int lane = threadIdx.x & 63;
+    if (lane < NG) xb[lane] = U;
+    FOTO_LDS_WAIT();
+    const int pb = (lane < NCO) ? 0 : NCO, m = lane - pb;
+    double X = 0.0;
+    if (lane < NG) {
+        if (m == 1) X += xb[pb];
+        if (m >= 2) X += 0.5 * xb[lane - 1];
+        if (m <= NCO - 3) X += 0.5 * xb[lane + 1];
+    }
+    FOTO_LDS_WAIT();
+    return (lane < NG) ? c0 * U + c1 * X : 0.0;
 }
 
-// next pass's scalars from the moments of (r_k, p_{k-1}); one thread.  scipy's loop:
-// top-of-iteration test ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p.
-__device__ __noinline__ void sstep2_plan(SStep& S, const double* Mrr, const double* Mrq, const double* Mqq, int maxiter) {
-    SPoly R = {{1.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-    SPoly P = {{0.0, 0.0, 0.0, 0.0}, {1.0, 0.0, 0.0, 0.0}};
+// Finish the pass's bookkeeping and plan the next pass (scipy's loop: top-of-iteration test
+// ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p).  Called by all 64
+// lanes of one wave with the same S (state at the start of the pass) and the summed
+// moments tot[NACC] (shared); lane 0 stores the new state.
+__device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* xb /* shared, 3 NG + 2 */, int init,
+                                double rtol, int maxiter) {
+    const int lane = threadIdx.x & 63;
+    if (init) {
+        S.k = 0;
+        S.rho_prev = 0.0;
+        S.atol = fmax(0.0, rtol * sqrt(tot[0]));   // scipy: max(atol, rtol * ||b||)
+        S.done = 0;
+        S.passes = 0;
+    } else {
+        S.k += S.nsteps;
+        if (S.fin) {
+            S.done = S.conv ? 1 : 2;
+            S.nsteps = 0;
+            if (lane == 0) *Sg = S;
+            return;
+        }
+    }
+    // row `lane` of H[a][c] = <T_a u, T_c v>, u, v in {r, q} by part: (M_{a+c} + M_{|a-c|}) / 2
+    // of family rr / rq / qq (degrees >= NMOM are never needed)
+    double hrow[NG];
+    {
+        const int a = lane < NG ? lane : 0, ia = a % NCO, pa = a / NCO;
+#pragma unroll
+        for (int c = 0; c < NG; ++c) {
+            const int ic = c % NCO, fam = pa + c / NCO;
+            const double* M = tot + fam * NMOM;
+            hrow[c] = (lane < NG && ia + ic < NMOM) ? 0.5 * (M[ia + ic] + M[ia > ic ? ia - ic : ic - ia]) : 0.0;
+        }
+    }
+    double R = (lane == 0) ? 1.0 : 0.0;     // r_k     = 1 * r
+    double P = (lane == NCO) ? 1.0 : 0.0;   // p_{k-1} = 1 * q
     double rho_prev = S.rho_prev;
     int n = 0;
     bool conv = false;
-    for (int i = 0; i < 2 && S.k + i < maxiter; ++i) {
-        const double rho = (i == 0) ? Mrr[0] : sp_ip(R, R, Mrr, Mrq, Mqq);
-        if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
-        SPoly Pn;
-        double beta = 0.0;
-        if (S.k + i == 0) {
-            Pn = R;
-        } else {
-            beta = rho / rho_prev;
-            for (int m = 0; m < 4; ++m) { Pn.r[m] = beta * P.r[m] + R.r[m]; Pn.q[m] = beta * P.q[m] + R.q[m]; }
+    for (int i = 0; i < SMAX; ++i) {
+        if (S.k + i >= maxiter) break;
+        double rho, cr = 0.0;
+        if (i == 0) rho = tot[0];
+        else {
+            rho = plan_ip(R, R, hrow, xb, &cr);
+            if (!(cr <= S_CLIM)) break;   // badly conditioned (or NaN): leave it to the next pass
         }
-        const SPoly Q = sp_mul_lam(Pn, S.c0, S.c1);
-        const double alpha = rho / sp_ip(Pn, Q, Mrr, Mrq, Mqq);
-        for (int m = 0; m < 4; ++m) { R.r[m] -= alpha * Q.r[m]; R.q[m] -= alpha * Q.q[m]; }
+        if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
+        const bool first = (S.k + i == 0);
+        const double beta = first ? 0.0 : rho / rho_prev;
+        const double Pn = first ? R : beta * P + R;
+        const double Q = plan_mul_lam(Pn, S.c0, S.c1, xb);
+        const double den = plan_ip(Pn, Q, hrow, xb, &cr);
+        if (i > 0 && !(cr <= S_CLIM)) break;
+        const double alpha = rho / den;
+        R = R - alpha * Q;
         P = Pn;
         rho_prev = rho;
-        S.a[i] = alpha;
-        S.b[i] = beta;
+        if (lane == 0) {
+            Sg->a[i] = alpha;
+            Sg->b[i] = beta;
+        }
         ++n;
     }
     S.nsteps = n;
     S.rho_prev = rho_prev;
+    S.passes += 1;
     S.fin = 0;
     S.conv = conv ? 1 : 0;
     if (conv || S.k + n >= maxiter) {
@@ -641,18 +756,12 @@ __device__ __noinline__ void sstep2_plan(SStep& S, const double* Mrr, const doub
         S.iters = conv ? S.k + n : maxiter;
         if (n == 0) S.done = conv ? 1 : 2;   // nothing left to apply
     }
+    if (lane == 0) {   // scalars only: a[], b[] were stored above
+        Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
+        Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
+    }
 }
 
-__device__ __forceinline__ void cheb_all(double x, double* T) {
-    T[0] = 1.0;
-    T[1] = x;
-#pragma unroll
-    for (int m = 2; m < SM; ++m) T[m] = 2.0 * x * T[m - 1] - T[m - 2];
-}
-
-// gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
-// last block stores this shard's moments at gath[rank * 21]; after the all-gather,
-// k_spec_s2_plan sums them in rank order and plans (identically on every rank).
 // element pair of tile t owned by this thread (see spec_for_each); n2 = 0: none
 struct SpElem {
     int64_t i;
@@ -680,47 +789,54 @@ __device__ __forceinline__ SpElem spec_elem(const SpecTab& T, int t, int ntx, in
     return e;
 }
 
-// gath == nullptr: single shard, the last block plans the next pass itself.  Otherwise the
-// last block stores this shard's moments at gath[rank * 21]; after the all-gather,
-// k_spec_s2_plan sums them in rank order and plans (identically on every rank).
-// A plain grid-stride tile loop: software-pipelining it (next tile's loads issued first)
-// measured 1 us slower -- the lam-table loads' waits drain the prefetch anyway.
+// gath == nullptr (FUSE): single shard, the last block plans the next pass itself.
+// Otherwise the last block stores this shard's moments at gath[rank * NACC]; after the
+// all-gather, k_spec_s2_plan sums them in rank order and plans (identically on every rank).
 #ifndef FOTO_S2_NTH
 #define FOTO_S2_NTH 256
 #endif
 constexpr int S2_NTH = FOTO_S2_NTH;   // threads per block of the s-step pass
 
+// 4 waves / SIMD: the streaming body needs the occupancy; the fused plan must fit beside it.
 template <bool VEC, bool INIT, bool FUSE>
-__global__ __launch_bounds__(S2_NTH) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
+__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
                                                     const double* __restrict__ bh, SStep* Sg, RedBuf rb,
                                                     double rtol, int maxiter, double* gath, int rank) {
     constexpr int TR = S2_NTH / 64;   // tile = TR rows x 128 columns
-    __shared__ SStep SS;
-    if (threadIdx.x == 0) SS = *Sg;
-    __syncthreads();
-    if (!INIT && (SS.done || SS.nsteps == 0)) return;
-    const int k = SS.k, ns = SS.nsteps;
-    const double a0 = SS.a[0], b0 = SS.b[0], a1 = SS.a[1], b1 = SS.b[1];
-    const double c0 = SS.c0, ic1 = 1.0 / SS.c1;
+    const SStep S0 = *Sg;             // uniform: scalar loads
+    if (!INIT && (S0.done || S0.nsteps == 0)) return;
+    const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
+    const double c0 = S0.c0, ic1 = 1.0 / S0.c1;
     const bool loadq = !INIT && k > 0;
     const double* src = INIT ? bh : rh;
-    double acc[3 * SM];
+    double acc[NACC];
 #pragma unroll
-    for (int m = 0; m < 3 * SM; ++m) acc[m] = 0.0;
+    for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
     auto moments = [&](double lam, double r, double q) {
-        double Tm[SM];
-        cheb_all((lam - c0) * ic1, Tm);
+        const double x = (lam - c0) * ic1, x2 = x + x;
         const double rr = r * r, rq = r * q, qq = q * q;
+        acc[0] += rr;
+        acc[NMOM] += rq;
+        acc[2 * NMOM] += qq;
+        acc[1] = fma(x, rr, acc[1]);
+        acc[NMOM + 1] = fma(x, rq, acc[NMOM + 1]);
+        acc[2 * NMOM + 1] = fma(x, qq, acc[2 * NMOM + 1]);
+        double tm2 = 1.0, tm1 = x;
 #pragma unroll
-        for (int m = 0; m < SM; ++m) {
-            acc[m] += Tm[m] * rr;
-            acc[SM + m] += Tm[m] * rq;
-            acc[2 * SM + m] += Tm[m] * qq;
+        for (int m = 2; m < NMOM; ++m) {
+            const double t = fma(x2, tm1, -tm2);
+            acc[m] = fma(t, rr, acc[m]);
+            acc[NMOM + m] = fma(t, rq, acc[NMOM + m]);
+            acc[2 * NMOM + m] = fma(t, qq, acc[2 * NMOM + m]);
+            tm2 = tm1;
+            tm1 = t;
         }
     };
     const int rows = T.Nt * T.nyl;
     const int ntx = (T.Nx + 127) / 128;
     const int ntiles = ntx * ((rows + TR - 1) / TR);
+    // A plain grid-stride tile loop: software-pipelining it (next tile's loads issued first)
+    // measured no faster at SMAX = 6 and spills at SMAX = 8 (tools/s2_ablation.hip).
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const SpElem e = spec_elem<TR>(T, t, ntx, rows);
         if (!e.n2) continue;
@@ -730,18 +846,15 @@ __global__ __launch_bounds__(S2_NTH) void k_spec_s2(SpecTab T, double* __restric
         if (INIT) {
             st2<VEC>(rh, e.i, e.n2, r0, r1);
         } else {
-            // step 0 (iteration k): scipy's p = beta p + r; r -= alpha (A p)
-            double p0 = (k == 0) ? r0 : b0 * q0 + r0;
-            double p1 = (k == 0) ? r1 : b0 * q1 + r1;
-            r0 = r0 - a0 * (e.l0 * p0);
-            r1 = r1 - a0 * (e.l1 * p1);
-            q0 = p0;
-            q1 = p1;
-            if (ns == 2) {   // step 1 (iteration k + 1)
-                p0 = b1 * q0 + r0;
-                p1 = b1 * q1 + r1;
-                r0 = r0 - a1 * (e.l0 * p0);
-                r1 = r1 - a1 * (e.l1 * p1);
+#pragma unroll
+            for (int i = 0; i < SMAX; ++i) {
+                if (i >= ns) break;
+                // iteration k + i: p = beta p + r (p = r at k = 0); r -= alpha (lam p)
+                const double a = S0.a[i], b = S0.b[i];
+                const double p0 = (k + i == 0) ? r0 : fma(b, q0, r0);
+                const double p1 = (k + i == 0) ? r1 : fma(b, q1, r1);
+                r0 = fma(-a, e.l0 * p0, r0);
+                r1 = fma(-a, e.l1 * p1, r1);
                 q0 = p0;
                 q1 = p1;
             }
@@ -751,58 +864,31 @@ __global__ __launch_bounds__(S2_NTH) void k_spec_s2(SpecTab T, double* __restric
         moments(e.l0, r0, q0);
         if (e.n2 == 2) moments(e.l1, r1, q1);
     }
-    __shared__ double tot[3 * SM];
-    if (sp_reduce_last_wide<3 * SM, S2_NTH>(acc, rb, tot) && threadIdx.x == 0) {
-        if (!FUSE) {
-            for (int m = 0; m < 3 * SM; ++m) gath[rank * 3 * SM + m] = tot[m];
-            return;
-        }
-        SStep S = SS;
-        if (INIT) {
-            S.k = 0;
-            S.rho_prev = 0.0;
-            S.atol = fmax(0.0, rtol * sqrt(tot[0]));   // scipy: max(atol, rtol * ||b||)
-            S.done = 0;
-        } else {
-            S.k = k + ns;
-            if (S.fin) {
-                S.done = S.conv ? 1 : 2;
-                S.nsteps = 0;
-                *Sg = S;
-                return;
-            }
-        }
-        sstep2_plan(S, tot, tot + SM, tot + 2 * SM, maxiter);
-        *Sg = S;
+    __shared__ double tot[NACC];
+    if (!sp_reduce_last_wide<NACC, S2_NTH>(acc, rb, tot)) return;
+    if (!FUSE) {
+        for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
+        return;
     }
+    if (threadIdx.x >= 64) return;
+    __shared__ double xb[3 * NG + 2];
+    sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
 }
 
-// Multi-shard planning step (one thread): moments summed over ranks in rank order.
-__global__ void k_spec_s2_plan(SStep* Sg, const double* __restrict__ gath, int world, int init, double rtol,
-                               int maxiter) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    SStep S = *Sg;
-    double tot[3 * SM];
-    for (int m = 0; m < 3 * SM; ++m) tot[m] = 0.0;
-    for (int g = 0; g < world; ++g)
-        for (int m = 0; m < 3 * SM; ++m) tot[m] += gath[g * 3 * SM + m];
-    if (init) {
-        S.k = 0;
-        S.rho_prev = 0.0;
-        S.atol = fmax(0.0, rtol * sqrt(tot[0]));
-        S.done = 0;
-    } else {
-        if (S.done || S.nsteps == 0) return;   // the pass did nothing
-        S.k = S.k + S.nsteps;
-        if (S.fin) {
-            S.done = S.conv ? 1 : 2;
-            S.nsteps = 0;
-            *Sg = S;
-            return;
-        }
+// Multi-shard planning step (one wave): moments summed over ranks in rank order.
+__global__ __launch_bounds__(64) void k_spec_s2_plan(SStep* Sg, const double* __restrict__ gath, int world, int init,
+                                                     double rtol, int maxiter) {
+    __shared__ double tot[NACC];
+    const SStep S0 = *Sg;
+    for (int m = threadIdx.x; m < NACC; m += 64) {
+        double s = 0.0;
+        for (int g = 0; g < world; ++g) s += gath[g * NACC + m];
+        tot[m] = s;
     }
-    sstep2_plan(S, tot, tot + SM, tot + 2 * SM, maxiter);
-    *Sg = S;
+    __syncthreads();
+    if (!init && S0.done) return;
+    __shared__ double xb[3 * NG + 2];
+    sstep_plan_wave(Sg, S0, tot, xb, init, rtol, maxiter);
 }
 
 // balanced contiguous split of n items over W parts (csrc/foto_bb.cpp split_planes)
@@ -851,12 +937,13 @@ struct SpecImpl {
     double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
     double *mx = nullptr, *my = nullptr, *mt = nullptr;
     RedBuf rb{};
-    double* gath = nullptr;       // s = 1: 2 doubles; s = 2 sharded: world * 21
+    double* gath = nullptr;       // s = 1: 2 doubles; s-step sharded: world * NACC
     CGScal* S = nullptr;
     CGScal* hS = nullptr;
     SStep* S2 = nullptr;
     SStep* hS2 = nullptr;
     int nblocks2 = 0;
+    int last_passes = 0;          // passes of the previous s-step solve (first chunk size)
     int sstep = 1;
     bool split_plan = false;
     std::vector<void*> allocs;
@@ -969,17 +1056,23 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     const int ntiles = ((g.Nx + 127) / 128) * ((rows + 3) / 4);
     P->nblocks = std::min(ntiles, 2048);
     {
+        // one resident wave of blocks: blocks per CU at the pass kernel's occupancy x CUs
         const int ntiles2 = ((g.Nx + 127) / 128) * ((rows + S2_NTH / 64 - 1) / (S2_NTH / 64));
+        int dev = 0, cus = 256, per_cu = 0;
+        FOTO_HIP_CHECK(hipGetDevice(&dev));
+        FOTO_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        FOTO_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spec_s2<true, false, true>, S2_NTH, 0));
         const char* e = getenv("FOTO_S2_BLOCKS");   // tuning knob for A/B runs
-        P->nblocks2 = std::min(ntiles2, e ? std::max(1, atoi(e)) : 256 * 1024 / S2_NTH);
+        const int want = e ? std::max(1, atoi(e)) : std::max(1, per_cu) * cus;
+        P->nblocks2 = std::min(ntiles2, want);
     }
-    const int cap = std::max(2 * P->nblocks, 3 * SM * P->nblocks2);
+    const int cap = std::max(2 * P->nblocks, NACC * P->nblocks2);
     FOTO_TRY(P->alloc(sizeof(double) * (cap + 8), &b));
     P->rb.partials = (double*)b;
     P->rb.ticket = (unsigned*)((double*)b + cap);
     P->rb.cap = cap;
     FOTO_HIP_CHECK(hipMemset(P->rb.ticket, 0, 8 * sizeof(double)));
-    FOTO_TRY(P->alloc(sizeof(double) * std::max(4, 3 * SM * world), &b)); P->gath = (double*)b;
+    FOTO_TRY(P->alloc(sizeof(double) * std::max(4, NACC * world), &b)); P->gath = (double*)b;
     FOTO_TRY(P->alloc(sizeof(CGScal), &b)); P->S = (CGScal*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
     FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
@@ -1058,7 +1151,8 @@ static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* i
         if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * N);
     }
     int passes = 0;
-    const int first = predicted > 6 ? (predicted - 4) / 2 : 4;
+    (void)predicted;
+    const int first = P->last_passes > 2 ? P->last_passes - 1 : 4;
     while (true) {
         const int chunk = (passes == 0) ? first : 1;
         for (int j = 0; j < chunk; ++j, ++passes) {
@@ -1076,6 +1170,7 @@ static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* i
     }
     *iters = P->hS2->iters;
     *info = (P->hS2->done == 1) ? 0 : maxiter;
+    P->last_passes = P->hS2->passes;
     return 0;
 }
 
@@ -1181,12 +1276,13 @@ int SpectralPlan::cg_plan(int init, double rtol, int maxiter, hipStream_t s) {
     return 0;
 }
 
-int SpectralPlan::poll(int* done, int* iters, hipStream_t s) {
+int SpectralPlan::poll(int* done, int* iters, int* passes, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
     FOTO_HIP_CHECK(hipStreamSynchronize(s));
     *done = P->hS2->done;
     *iters = P->hS2->iters;
+    *passes = P->hS2->passes;
     return 0;
 }
 
@@ -1218,7 +1314,7 @@ double* SpectralPlan::stage() const { return ((SpecImpl*)impl)->stage; }
 double* SpectralPlan::box_in() const { return ((SpecImpl*)impl)->tmp; }
 double* SpectralPlan::box_out() const { return ((SpecImpl*)impl)->rh; }
 double* SpectralPlan::gath() const { return ((SpecImpl*)impl)->gath; }
-int SpectralPlan::moments() { return 3 * SM; }
+int SpectralPlan::moments() { return NACC; }
 int SpectralPlan::y0() const { return ((SpecImpl*)impl)->y0; }
 int SpectralPlan::nyl() const { return ((SpecImpl*)impl)->nyl; }
 
