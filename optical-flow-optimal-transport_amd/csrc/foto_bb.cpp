@@ -354,9 +354,9 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));
     int passes = 0, done = 0, its = 0, planned = 0;
-    const int first = c->last_passes > 2 ? c->last_passes - 1 : 4;
+    const int first = c->last_passes > 0 ? c->last_passes + 2 : 8;   // over-predict (see solve_s2)
     while (true) {
-        const int chunk = (passes == 0) ? first : 1;
+        const int chunk = (passes == 0) ? first : 2;
         for (int j = 0; j < chunk; ++j, ++passes) {
             for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_pass(rtol, maxiter, kt, c->s));
             FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
@@ -376,6 +376,7 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     *info = (done == 1) ? 0 : maxiter;
     c->last_cg = its;
     c->last_passes = planned;
+    kt->discard_last(FOTO_K_SPEC, std::max(0, passes - planned) * (int)c->sh.size());   // no-op passes
     return 0;
 }
 

@@ -99,6 +99,17 @@ struct KTimer {
         (void)hipEventRecord(b, s);
         pend.push_back({a, b, cls, by});
     }
+    // drop the `count` most recent pending records of class cls (launches that turned out to
+    // be no-ops, e.g. s-step passes enqueued after the solve had finished)
+    void discard_last(int cls, int count) {
+        for (int i = (int)pend.size() - 1; i >= 0 && count > 0; --i) {
+            if (pend[i].cls != cls) continue;
+            pool.push_back(pend[i].a);
+            pool.push_back(pend[i].b);
+            pend.erase(pend.begin() + i);
+            --count;
+        }
+    }
     void resolve() {   // call after a stream sync
         for (auto& p : pend) {
             float t = 0.f;

@@ -3,17 +3,21 @@
 profiles/<tag>_*.md / .json, and write profiles/pmc_traffic.json (HBM bytes per launch of
 each hot kernel) that bench.py reports as roofline.traffic.
 
-HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), following
-MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts 64 B per 128-B request of a
-coalesced streaming read (report = 1/2 of the bytes); WRITE_SIZE is exact for streaming
-stores.  Our kernels read fp64 with 8-16 B per lane, fully coalesced.
+HBM bytes per launch = f_load * FETCH_SIZE + f_store * WRITE_SIZE (KiB -> bytes).  The
+correction factors come from a calibration run of tools/calib_fetch (known byte counts,
+2 GiB streams far beyond the Infinity Cache) under the same two PMC passes.  Measured
+(profiles/r01c_*): FETCH_SIZE reports 1/2 of the bytes of a streaming read for 8-B and
+16-B loads per lane alike (MI355X_MICROARCH.md HBM section states it for 16 B); WRITE_SIZE
+is exact.  Each kernel's factor follows the load width it uses (LOAD_WIDTH below).
 
 usage: tools/summarize_profile.py --tag r01 --kt gpurun_out/prof_kt --fetch gpurun_out/prof_fetch \
-          --write gpurun_out/prof_write [--bench gpurun_out/bench_full.log]
+          --write gpurun_out/prof_write --calib-fetch gpurun_out/cal_fetch --calib-write gpurun_out/cal_write \
+          [--bench gpurun_out/bench_full.log]
 """
 import argparse
 import collections
 import csv
+import glob
 import json
 import os
 
@@ -21,6 +25,19 @@ SHORT = {
     "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox": "prox", "k_rhs": "rhs", "k_spec": "spec_cg",
     "k_dct": "dct", "k_traj": "flow", "k_gn_pcg_dir": "gn_dir", "k_gn_pcg_upd": "gn_upd",
 }
+
+
+# bytes per lane of each hot kernel's streaming loads (csrc/*.hip)
+LOAD_WIDTH = {"spec_cg": 16, "cg_upd": 8, "cg_dir": 8, "prox": 8, "rhs": 8, "dct": 8, "flow": 8,
+              "gn_dir": 8, "gn_upd": 8}
+CALIB_BYTES = {"rd8": 2 << 30, "rd16": 2 << 30, "wr8": 1 << 30, "wr16": 1 << 30}
+
+
+def find_csv(dirname, suffix):
+    hits = sorted(glob.glob(os.path.join(dirname, "**", "*" + suffix), recursive=True))
+    if not hits:
+        raise FileNotFoundError(f"no *{suffix} under {dirname}")
+    return hits[0]
 
 
 def short(name):
@@ -32,8 +49,7 @@ def short(name):
 
 def pmc(dirname, counter):
     agg = collections.defaultdict(list)
-    path = os.path.join(dirname, "run_counter_collection.csv")
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(open(find_csv(dirname, "counter_collection.csv"))):
         if r["Counter_Name"] == counter:
             agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
@@ -45,11 +61,13 @@ def main():
     ap.add_argument("--kt", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--calib-fetch")
+    ap.add_argument("--calib-write")
     ap.add_argument("--bench")
     ap.add_argument("--out", default="profiles")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    rows = list(csv.DictReader(open(os.path.join(a.kt, "run_kernel_stats.csv"))))
+    rows = list(csv.DictReader(open(find_csv(a.kt, "kernel_stats.csv"))))
     lines = [f"# rocprofv3 kernel stats ({a.tag})", "",
              "| kernel | calls | total ms | avg us | min us | max us | % |", "|---|---|---|---|---|---|---|"]
     stats = {}
@@ -61,16 +79,30 @@ def main():
                      f"{float(r['AverageNs'])/1e3:.2f} | {float(r['MinNs'])/1e3:.2f} | "
                      f"{float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.2f} |")
     traffic = {}
+    fac_ld, fac_st = {8: 1.0, 16: 2.0}, 1.0   # defaults (guide); replaced by the calibration
+    if a.calib_fetch and a.calib_write:
+        cf, _ = pmc(a.calib_fetch, "FETCH_SIZE")
+        cw, _ = pmc(a.calib_write, "WRITE_SIZE")
+        fac_ld = {8: CALIB_BYTES["rd8"] / (cf["rd8"] * 1024.0), 16: CALIB_BYTES["rd16"] / (cf["rd16"] * 1024.0)}
+        fac_st = 0.5 * (CALIB_BYTES["wr8"] / (cw["wr8"] * 1024.0) + CALIB_BYTES["wr16"] / (cw["wr16"] * 1024.0))
+        lines += ["", "## PMC calibration (tools/calib_fetch, 2 GiB streams)", "",
+                  "| access | bytes | counter KiB | bytes / counter byte |", "|---|---|---|---|"]
+        for k in ("rd8", "rd16"):
+            lines.append(f"| {k} | {CALIB_BYTES[k]} | {cf[k]:.0f} | {CALIB_BYTES[k] / (cf[k] * 1024.0):.3f} |")
+        for k in ("wr8", "wr16"):
+            lines.append(f"| {k} | {CALIB_BYTES[k]} | {cw[k]:.0f} | {CALIB_BYTES[k] / (cw[k] * 1024.0):.3f} |")
     if a.fetch and a.write:
         f, nf = pmc(a.fetch, "FETCH_SIZE")
         w, nw = pmc(a.write, "WRITE_SIZE")
-        lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
-                  "| kernel | launches | FETCH_SIZE KiB | WRITE_SIZE KiB | HBM MB/launch (2F+W) |",
-                  "|---|---|---|---|---|"]
+        lines += ["", "## HBM traffic per launch (PMC, separate passes, calibrated per load width)", "",
+                  "| kernel | launches | FETCH_SIZE KiB | WRITE_SIZE KiB | load B/lane | HBM MB/launch |",
+                  "|---|---|---|---|---|---|"]
         for k in sorted(set(f) & set(w)):
-            hbm = (2 * f[k] + w[k]) * 1024.0
-            traffic[k] = {"fetch_kib": f[k], "write_kib": w[k], "hbm_bytes_per_launch": hbm, "launches": nf[k]}
-            lines.append(f"| {k} | {nf[k]} | {f[k]:.0f} | {w[k]:.0f} | {hbm/1e6:.1f} |")
+            lw = LOAD_WIDTH.get(k, 8)
+            hbm = (fac_ld[lw] * f[k] + fac_st * w[k]) * 1024.0
+            traffic[k] = {"fetch_kib": f[k], "write_kib": w[k], "load_width": lw, "fetch_factor": fac_ld[lw],
+                          "store_factor": fac_st, "hbm_bytes_per_launch": hbm, "launches": nf[k]}
+            lines.append(f"| {k} | {nf[k]} | {f[k]:.0f} | {w[k]:.0f} | {lw} | {hbm/1e6:.1f} |")
     if a.bench and os.path.exists(a.bench):
         for ln in open(a.bench):
             if ln.startswith("{"):
