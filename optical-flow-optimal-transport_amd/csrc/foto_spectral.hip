@@ -16,8 +16,10 @@
 #include <cmath>
 #include <cstdlib>
 #include <memory>
+#include <vector>
 
 #include "foto_spectral.h"
+#include "foto_twiddles.h"
 
 namespace foto {
 
@@ -424,6 +426,322 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
     }
     return hipGetLastError();
 }
+
+// ============================================================================ DCT along one axis (FFT)
+//
+// Orthonormal DCT-II (forward) / DCT-III (inverse) of real lines of even length N = 2M
+// through a length-M complex DFT (Makhoul's reordering): v = (x0, x2, x4, ..., x5, x3, x1),
+// z_j = v_2j + i v_2j+1, Z = DFT_M(z), then with C_k = conj Z_{(M-k) mod M}
+//     V_k = (Z_k + C_k) / 2 + e^{-2 pi i k/N} (Z_k - C_k) / (2i)      (= DFT_N(v)_k)
+//     Y_k = e^{-i pi k/(2N)} V_k,   X_k = s_k Re Y_k,   X_{N-k} = -s_{N-k} Im Y_k,
+// s_0 = sqrt(1/N), s_k = sqrt(2/N).  The inverse runs the same steps backwards (V from X by
+// Hermitian symmetry, Z_k = Ve_k + i Vo_k, z = IDFT_M(Z), x from v).  DFT_M is two-stage
+// Cooley-Tukey, M = M1 M2: M2 DFTs of length M1 over the stride-M2 subsequences, twiddle
+// e^{-2 pi i j2 k1 / M}, M1 DFTs of length M2; the small DFTs are direct with compile-time
+// roots (foto_twiddles.h), so multiplications by 0 / +-1 fold away.  About 2 (M1 + M2) + 8
+// fp64 FMA per element (75 at N = 640) instead of the GEMM's N; each axis pass reads and
+// writes the volume once.  LPB lines per block are staged in LDS; transforms are in place
+// within a line.  Lines are contiguous rows (CONTIG, the x axis) or strided columns (y, t)
+// taken LPB consecutive columns at a time so global loads and stores stay coalesced.
+//
+// Per-axis table (fp64): WM[2M] = e^{-2 pi i p/M}, PA[2(M+1)] = e^{-2 pi i k/N},
+// PB[2(M+1)] = e^{-i pi k/(2N)}, then s_0, s.
+
+template <int M1, int M2>
+struct FftGeom {
+    static constexpr int M = M1 * M2, N = 2 * M;
+    // lines per block: LDS (lines + twiddles) <= 64 KB
+    static constexpr int lpb() {
+        const int c[8] = {64, 32, 16, 12, 8, 4, 2, 1};
+        for (int i = 0; i < 8; ++i)
+            if (c[i] * N * 8 + 16 * M <= 65536) return c[i];
+        return 1;
+    }
+    static constexpr int LPB = lpb();
+    static constexpr int TAB = 6 * M + 6;
+};
+
+template <int R, bool INV>
+__device__ __forceinline__ constexpr double root_re(int p) { return Roots<R>::re[p]; }
+template <int R, bool INV>
+__device__ __forceinline__ constexpr double root_im(int p) { return INV ? -Roots<R>::im[p] : Roots<R>::im[p]; }
+
+// acc += x * w (complex) with w a compile-time root: zero / unit parts fold away
+template <int R, bool INV>
+__device__ __forceinline__ void cmac_root(double& ar, double& ai, double xr, double xi, int p) {
+    const double wr = root_re<R, INV>(p), wi = root_im<R, INV>(p);
+    if (wr == 1.0) { ar += xr; ai += xi; }
+    else if (wr == -1.0) { ar -= xr; ai -= xi; }
+    else if (wr != 0.0) { ar = fma(xr, wr, ar); ai = fma(xi, wr, ai); }
+    if (wi == 1.0) { ar -= xi; ai += xr; }
+    else if (wi == -1.0) { ar += xi; ai -= xr; }
+    else if (wi != 0.0) { ar = fma(-xi, wi, ar); ai = fma(xr, wi, ai); }
+}
+
+// stage 1 (in place on the LDS lines): for each (line, j2): the length-M1 DFT of
+// z[M2 j1 + j2], times e^{-+2 pi i j2 k1 / M}, stored at M2 k1 + j2
+template <int M1, int M2, bool INV, int LPB>
+__device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
+    constexpr int M = M1 * M2, N = 2 * M;
+    for (int task = threadIdx.x; task < LPB * M2; task += 256) {
+        const int l = task / M2, j2 = task - (task / M2) * M2;
+        double* Ll = L + l * N;
+        double xr[M1], xi[M1];
+#pragma unroll
+        for (int j1 = 0; j1 < M1; ++j1) {
+            xr[j1] = Ll[2 * (M2 * j1 + j2)];
+            xi[j1] = Ll[2 * (M2 * j1 + j2) + 1];
+        }
+#pragma unroll
+        for (int k1 = 0; k1 < M1; ++k1) {
+            double ar = 0.0, ai = 0.0;
+#pragma unroll
+            for (int j1 = 0; j1 < M1; ++j1) cmac_root<M1, INV>(ar, ai, xr[j1], xi[j1], (j1 * k1) % M1);
+            const int q = j2 * k1;   // < M
+            const double tr = TW[2 * q], ti = INV ? -TW[2 * q + 1] : TW[2 * q + 1];
+            Ll[2 * (M2 * k1 + j2)] = fma(ar, tr, -ai * ti);
+            Ll[2 * (M2 * k1 + j2) + 1] = fma(ar, ti, ai * tr);
+        }
+    }
+}
+
+// stage 2 (in place): for each (line, k1): the length-M2 DFT of the row M2 k1 + j2; element
+// k = k1 + M1 k2 of the result lands at position M2 k1 + k2
+template <int M1, int M2, bool INV, int LPB>
+__device__ __forceinline__ void fft_stage2(double* L) {
+    constexpr int M = M1 * M2, N = 2 * M;
+    for (int task = threadIdx.x; task < LPB * M1; task += 256) {
+        const int l = task / M1, k1 = task - (task / M1) * M1;
+        double* Lr = L + l * N + 2 * M2 * k1;
+        double xr[M2], xi[M2];
+#pragma unroll
+        for (int j2 = 0; j2 < M2; ++j2) {
+            xr[j2] = Lr[2 * j2];
+            xi[j2] = Lr[2 * j2 + 1];
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < M2; ++k2) {
+            double ar = 0.0, ai = 0.0;
+#pragma unroll
+            for (int j2 = 0; j2 < M2; ++j2) cmac_root<M2, INV>(ar, ai, xr[j2], xi[j2], (j2 * k2) % M2);
+            Lr[2 * k2] = ar;
+            Lr[2 * k2 + 1] = ai;
+        }
+    }
+}
+
+template <int M1, int M2>
+__device__ __forceinline__ int fft_pos(int k) { return M2 * (k % M1) + k / M1; }   // where Z_k lands
+
+struct FftLines {   // this block's lines: CONTIG rows o0 + l, or columns (o0, i0 + l) of stride `inner`
+    int o0, i0, nl;
+};
+
+template <bool CONTIG, int LPB>
+__device__ __forceinline__ FftLines fft_lines(int outer, int inner) {
+    FftLines f;
+    if (CONTIG) {
+        f.o0 = blockIdx.x * LPB;
+        f.i0 = 0;
+        f.nl = min(LPB, outer - f.o0);
+    } else {
+        const int nib = (inner + LPB - 1) / LPB;
+        f.o0 = blockIdx.x / nib;
+        f.i0 = (blockIdx.x - f.o0 * nib) * LPB;
+        f.nl = min(LPB, inner - f.i0);
+    }
+    return f;
+}
+
+template <int M1, int M2, bool CONTIG>
+__global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
+                                                     const double* __restrict__ in, double* __restrict__ out) {
+    using G = FftGeom<M1, M2>;
+    constexpr int M = G::M, N = G::N, LPB = G::LPB;
+    __shared__ double L[LPB * N];
+    __shared__ double TW[2 * M];
+    const int tid = threadIdx.x;
+    const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
+    const int64_t st = CONTIG ? 1 : inner;
+    auto base = [&](int l) -> int64_t {
+        return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
+    };
+    for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
+    for (int idx = tid; idx < LPB * N; idx += 256) {   // load, Makhoul order
+        int l, j;
+        if (CONTIG) { l = idx / N; j = idx - l * N; }
+        else { j = idx / LPB; l = idx - j * LPB; }
+        const double x = (l < f.nl) ? in[base(l) + j * st] : 0.0;
+        L[l * N + ((j & 1) ? N - 1 - (j >> 1) : (j >> 1))] = x;
+    }
+    __syncthreads();
+    fft_stage1<M1, M2, false, LPB>(L, TW);
+    __syncthreads();
+    fft_stage2<M1, M2, false, LPB>(L);
+    __syncthreads();
+    const double* PA = tab + 2 * M;
+    const double* PB = PA + 2 * (M + 1);
+    const double s0 = PB[2 * (M + 1)], s = PB[2 * (M + 1) + 1];
+    for (int idx = tid; idx < LPB * (M + 1); idx += 256) {
+        int l, k;
+        if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
+        else { k = idx / LPB; l = idx - k * LPB; }
+        if (l >= f.nl) continue;
+        const double* Ll = L + l * N;
+        const int pa = 2 * fft_pos<M1, M2>(k == M ? 0 : k), pb = 2 * fft_pos<M1, M2>(k == 0 ? 0 : M - k);
+        const double zr = Ll[pa], zi = Ll[pa + 1], cr = Ll[pb], ci = -Ll[pb + 1];
+        const double er = 0.5 * (zr + cr), ei = 0.5 * (zi + ci);     // DFT of the even samples
+        const double orr = 0.5 * (zi - ci), oi = 0.5 * (cr - zr);     // DFT of the odd samples
+        const double war = PA[2 * k], wai = PA[2 * k + 1];
+        const double vr = er + fma(war, orr, -wai * oi), vi = ei + fma(war, oi, wai * orr);
+        const double wbr = PB[2 * k], wbi = PB[2 * k + 1];
+        const double yr = fma(wbr, vr, -wbi * vi), yi = fma(wbr, vi, wbi * vr);
+        const int64_t b = base(l);
+        out[b + k * st] = (k == 0 ? s0 : s) * yr;
+        if (k > 0 && k < M) out[b + (N - k) * st] = -s * yi;
+    }
+}
+
+template <int M1, int M2, bool CONTIG>
+__global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const double* __restrict__ tab,
+                                                     const double* __restrict__ in, double* __restrict__ out) {
+    using G = FftGeom<M1, M2>;
+    constexpr int M = G::M, N = G::N, LPB = G::LPB;
+    constexpr int TPT = (LPB * M + 255) / 256;   // pre-process tasks per thread
+    __shared__ double L[LPB * N];
+    __shared__ double TW[2 * M];
+    const int tid = threadIdx.x;
+    const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
+    const int64_t st = CONTIG ? 1 : inner;
+    auto base = [&](int l) -> int64_t {
+        return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
+    };
+    for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
+    for (int idx = tid; idx < LPB * N; idx += 256) {   // load X, natural order
+        int l, j;
+        if (CONTIG) { l = idx / N; j = idx - l * N; }
+        else { j = idx / LPB; l = idx - j * LPB; }
+        L[l * N + j] = (l < f.nl) ? in[base(l) + j * st] : 0.0;
+    }
+    __syncthreads();
+    const double* PA = tab + 2 * M;
+    const double* PB = PA + 2 * (M + 1);
+    const double is0 = 1.0 / PB[2 * (M + 1)], is = 1.0 / PB[2 * (M + 1) + 1];
+    double Zr[TPT], Zi[TPT];
+#pragma unroll
+    for (int t = 0; t < TPT; ++t) {
+        const int idx = tid + 256 * t;
+        Zr[t] = Zi[t] = 0.0;
+        if (idx >= LPB * M) continue;
+        const int l = idx / M, k = idx - (idx / M) * M;
+        const double* Ll = L + l * N;
+        // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
+        auto V = [&](int j, double& vr, double& vi) {
+            const double yr = Ll[j] * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -Ll[N - j] * is;
+            const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
+            vr = fma(wbr, yr, -wbi * yi);
+            vi = fma(wbr, yi, wbi * yr);
+        };
+        double ar, ai, br, bi;
+        V(k, ar, ai);
+        V(M - k, br, bi);
+        bi = -bi;                                                  // conj V_{M-k} = V_{k+M}
+        const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_k
+        const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
+        const double war = PA[2 * k], wai = -PA[2 * k + 1];        // e^{+2 pi i k/N}
+        const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_k
+        Zr[t] = er - oi;                                           // Z = Ve + i Vo
+        Zi[t] = ei + orr;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TPT; ++t) {
+        const int idx = tid + 256 * t;
+        if (idx >= LPB * M) continue;
+        const int l = idx / M, k = idx - (idx / M) * M;
+        L[l * N + 2 * k] = Zr[t];
+        L[l * N + 2 * k + 1] = Zi[t];
+    }
+    __syncthreads();
+    fft_stage1<M1, M2, true, LPB>(L, TW);
+    __syncthreads();
+    fft_stage2<M1, M2, true, LPB>(L);
+    __syncthreads();
+    constexpr double iM = 1.0 / M;
+    for (int idx = tid; idx < LPB * N; idx += 256) {   // x_i = v_p, p = Makhoul position of i
+        int l, i;
+        if (CONTIG) { l = idx / N; i = idx - l * N; }
+        else { i = idx / LPB; l = idx - i * LPB; }
+        if (l >= f.nl) continue;
+        const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
+        out[base(l) + i * st] = L[l * N + 2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
+    }
+}
+
+// supported line lengths N = 2 M1 M2 (others use the GEMM kernels)
+#define FOTO_FFT_SIZES(X) X(8, 2, 2) X(16, 2, 4) X(32, 4, 4) X(64, 4, 8) X(128, 8, 8) X(256, 8, 16) \
+    X(480, 15, 16) X(512, 16, 16) X(640, 16, 20) X(1024, 16, 32)
+
+static bool fft_factors(int n, int* m1, int* m2) {
+#define FOTO_FFT_CASE(NN, A, B) if (n == NN) { *m1 = A; *m2 = B; return true; }
+    FOTO_FFT_SIZES(FOTO_FFT_CASE)
+#undef FOTO_FFT_CASE
+    return false;
+}
+
+// per-axis table (host, long double): see the layout above
+static std::vector<double> fft_table(int n) {
+    const int M = n / 2;
+    std::vector<double> t;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int p = 0; p < M; ++p) {
+        t.push_back((double)cosl(2.0L * pi * p / M));
+        t.push_back((double)-sinl(2.0L * pi * p / M));
+    }
+    for (int k = 0; k <= M; ++k) {
+        t.push_back((double)cosl(2.0L * pi * k / n));
+        t.push_back((double)-sinl(2.0L * pi * k / n));
+    }
+    for (int k = 0; k <= M; ++k) {
+        t.push_back((double)cosl(pi * k / (2.0L * n)));
+        t.push_back((double)-sinl(pi * k / (2.0L * n)));
+    }
+    t.push_back((double)sqrtl(1.0L / n));
+    t.push_back((double)sqrtl(2.0L / n));
+    return t;
+}
+
+static int g_dct_fft = -1;   // FOTO_DCT_FFT=0 selects the GEMM kernels (A/B runs)
+
+// FFT path along one axis of [outer][n][inner]; hipErrorNotSupported if n has no instantiation
+static hipError_t dct_fft_axis(int outer, int n, int inner, bool inv, const double* tab, const double* in,
+                               double* out, hipStream_t s) {
+    if (g_dct_fft < 0) {
+        const char* e = getenv("FOTO_DCT_FFT");
+        g_dct_fft = e ? atoi(e) : 1;
+    }
+    int m1, m2;
+    // n < 64: the GEMM kernel is as fast (t axis at 32: 49 vs 54 us)
+    if (!g_dct_fft || !tab || n < 64 || !fft_factors(n, &m1, &m2)) return hipErrorNotSupported;
+#define FOTO_FFT_LAUNCH(NN, A, B)                                                                  \
+    if (n == NN) {                                                                                 \
+        constexpr int LPB = FftGeom<A, B>::LPB;                                                    \
+        const bool contig = (inner == 1);                                                          \
+        const int nb = contig ? (outer + LPB - 1) / LPB : outer * ((inner + LPB - 1) / LPB);       \
+        if (contig) {                                                                              \
+            if (inv) k_dct_fft_inv<A, B, true><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);     \
+            else k_dct_fft_fwd<A, B, true><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);         \
+        } else {                                                                                   \
+            if (inv) k_dct_fft_inv<A, B, false><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);    \
+            else k_dct_fft_fwd<A, B, false><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);        \
+        }                                                                                          \
+        return hipGetLastError();                                                                  \
+    }
+    FOTO_FFT_SIZES(FOTO_FFT_LAUNCH)
+#undef FOTO_FFT_LAUNCH
+    return hipErrorNotSupported;
+}
+
 
 // ============================================================================ CG in the eigenbasis
 
@@ -936,6 +1254,7 @@ struct SpecImpl {
     double *tmpp = nullptr, *stage = nullptr;                               // physical slab scratch
     double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
     double *mx = nullptr, *my = nullptr, *mt = nullptr;
+    double *Fx = nullptr, *Fy = nullptr, *Ft = nullptr;   // FFT-DCT tables (nullptr: GEMM path)
     RedBuf rb{};
     double* gath = nullptr;       // s = 1: 2 doubles; s-step sharded: world * NACC
     CGScal* S = nullptr;
@@ -1048,6 +1367,19 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     const double my_max = mu.back();
     FOTO_TRY(up(g.Nt, &P->Ct, &P->CtT, &P->mt));
     const double mt_max = mu.back();
+    auto upf = [&](int n, double** Fd) -> int {
+        int m1, m2;
+        if (!fft_factors(n, &m1, &m2)) return 0;
+        const std::vector<double> t = fft_table(n);
+        void* p;
+        FOTO_TRY(P->alloc(t.size() * 8, &p));
+        *Fd = (double*)p;
+        FOTO_HIP_CHECK(hipMemcpy(*Fd, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+        return 0;
+    };
+    FOTO_TRY(upf(g.Nx, &P->Fx));
+    FOTO_TRY(upf(g.Ny, &P->Fy));
+    FOTO_TRY(upf(g.Nt, &P->Ft));
     // Chebyshev scaling of lam: global spectrum bounds (identical on every rank)
     const double lmin = r * eps, lmax = r * eps + r * (mt_max + my_max + mx_max);
     P->c0 = 0.5 * (lmax + lmin);
@@ -1083,15 +1415,26 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
 
 SpectralPlan::~SpectralPlan() { delete (SpecImpl*)impl; }
 
+// one axis of [outer][n][inner]: FFT kernels where the length has an instantiation, GEMM otherwise
+static hipError_t dct_pass(const SpecImpl* P, int axis, bool inv, int outer, int inner, const double* in, double* out,
+                           hipStream_t s) {
+    const double* tab = axis == 0 ? P->Fx : axis == 1 ? P->Fy : P->Ft;
+    const int n = axis == 0 ? P->g.Nx : axis == 1 ? P->g.Ny : P->g.Nt;
+    const hipError_t e = dct_fft_axis(outer, n, inner, inv, tab, in, out, s);
+    if (e != hipErrorNotSupported) return e;
+    const double* C = axis == 0 ? (inv ? P->CxT : P->Cx) : axis == 1 ? (inv ? P->CyT : P->Cy) : (inv ? P->CtT : P->Ct);
+    return dct_axis(outer, n, inner, C, in, out, s);
+}
+
 // 3-D transforms of a single shard: forward = (Ct (x) Cy (x) Cx), inverse = transpose.
 static int forward3(SpecImpl* P, double* in, double* scratch, double* out, KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     // in -x-> scratch -y-> in -t-> out   (in is clobbered)
-    FOTO_HIP_CHECK(dct_axis(g.Nt * g.Ny, g.Nx, 1, P->Cx, in, scratch, s));
-    FOTO_HIP_CHECK(dct_axis(g.Nt, g.Ny, g.Nx, P->Cy, scratch, in, s));
-    FOTO_HIP_CHECK(dct_axis(1, g.Nt, (int)g.nxy, P->Ct, in, out, s));
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, in, scratch, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, scratch, in, s));
+    FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, (int)g.nxy, in, out, s));
     if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
     return 0;
 }
@@ -1101,9 +1444,9 @@ static int inverse3(SpecImpl* P, double* in, double* scratch, double* out, KTime
     const double N = (double)g.Nt * (double)g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     // in -t-> scratch -y-> in -x-> out   (in is clobbered)
-    FOTO_HIP_CHECK(dct_axis(1, g.Nt, (int)g.nxy, P->CtT, in, scratch, s));
-    FOTO_HIP_CHECK(dct_axis(g.Nt, g.Ny, g.Nx, P->CyT, scratch, in, s));
-    FOTO_HIP_CHECK(dct_axis(g.Nt * g.Ny, g.Nx, 1, P->CxT, in, out, s));
+    FOTO_HIP_CHECK(dct_pass(P, 2, true, 1, (int)g.nxy, in, scratch, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, scratch, in, s));
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, in, out, s));
     if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
     return 0;
 }
@@ -1241,8 +1584,8 @@ int SpectralPlan::fwd_local(double* b, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_axis(g.nloc * g.Ny, g.Nx, 1, P->Cx, b, P->tmpp, s));      // x
-    FOTO_HIP_CHECK(dct_axis(g.nloc, g.Ny, g.Nx, P->Cy, P->tmpp, b, s));          // y
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.nloc * g.Ny, 1, b, P->tmpp, s));      // x
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.nloc, g.Nx, P->tmpp, b, s));          // y
     const int64_t n = (int64_t)g.nloc * g.nxy;
     k_spec_pack<true><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world, b,
                                                                                      P->stage);
@@ -1255,7 +1598,7 @@ int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_axis(1, g.Nt, P->nyl * g.Nx, P->Ct, P->tmp, P->bh, s));   // box tmp -> b^
+    FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, P->nyl * g.Nx, P->tmp, P->bh, s));   // box tmp -> b^
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
     return 0;
 }
@@ -1299,7 +1642,7 @@ int SpectralPlan::inv_t(KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(launch_xhat(P, s));                                              // tmp = x^
-    FOTO_HIP_CHECK(dct_axis(1, g.Nt, P->nyl * g.Nx, P->CtT, P->tmp, P->rh, s));    // rh = box of x~
+    FOTO_HIP_CHECK(dct_pass(P, 2, true, 1, P->nyl * g.Nx, P->tmp, P->rh, s));    // rh = box of x~
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
     return 0;
 }
@@ -1312,8 +1655,8 @@ int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t 
     k_spec_pack<false><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world,
                                                                                       scratch, P->stage);
     FOTO_HIP_CHECK(hipGetLastError());
-    FOTO_HIP_CHECK(dct_axis(g.nloc, g.Ny, g.Nx, P->CyT, scratch, P->tmpp, s));     // y
-    FOTO_HIP_CHECK(dct_axis(g.nloc * g.Ny, g.Nx, 1, P->CxT, P->tmpp, x, s));       // x
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.nloc, g.Nx, scratch, P->tmpp, s));     // y
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.nloc * g.Ny, 1, P->tmpp, x, s));       // x
     if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
     return 0;
 }
