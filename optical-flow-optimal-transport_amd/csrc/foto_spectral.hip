@@ -139,6 +139,149 @@ __device__ __forceinline__ double sp_seg_total(const double* red2, int k) {
     return s + c;
 }
 
+// ---------------------------------------------------------------------------- reduce-scatter
+// Wave-level sum of K per-lane values without LDS: at each xor level a lane keeps one half
+// of its remaining values and adds the partner's copy of that half (the partner sends it),
+// so the K values halve per level (48 -> 24 -> 12 -> 6 -> 3 over xor 32, 16, 8, 4) and the
+// last levels butterfly the remainder.  Lane l ends with the wave totals of quantities
+// rs_base(l) + j, j < rs_count<K>(); lanes differing only in the butterflied low bits hold
+// identical values.  Every total is a pairwise tree over the 64 lanes: deterministic, and
+// (measured in the s-step prototype) as accurate as compensated summation for the moments.
+template <int K>
+constexpr int rs_levels() {   // halving levels
+    int c = K, l = 0;
+    while (c % 2 == 0 && l < 6) { c /= 2; ++l; }
+    return l;
+}
+template <int K>
+constexpr int rs_count() { return K >> rs_levels<K>(); }
+
+template <int C, int MASK>
+__device__ __forceinline__ void rs_halve(double* v, int lane) {
+    if constexpr (C % 2 == 0 && MASK >= 1) {
+        const bool hi = (lane & MASK) != 0;
+#pragma unroll
+        for (int j = 0; j < C / 2; ++j) {
+            if (j % 8 == 0) asm volatile("" ::: "memory");   // bound batched shuffles (registers)
+            const double send = hi ? v[j] : v[C / 2 + j];
+            const double keep = hi ? v[C / 2 + j] : v[j];
+            v[j] = keep + __shfl_xor(send, MASK, 64);
+        }
+        rs_halve<C / 2, MASK / 2>(v, lane);
+    } else if constexpr (MASK >= 1) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] += __shfl_xor(v[j], MASK, 64);
+        rs_halve<C, MASK / 2>(v, lane);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ int rs_base(int lane) {
+    int base = 0, c = K;
+#pragma unroll
+    for (int l = 0, mask = 32; l < rs_levels<K>(); ++l, mask >>= 1) {
+        c /= 2;
+        if (lane & mask) base += c;
+    }
+    return base;
+}
+
+// Block (NTH threads) sum of K values per thread into red[k] (shared, K): reduce-scatter per
+// wave, then the waves' partials are added pairwise by K threads.  wred: shared, (NTH/64) * K.
+template <int K, int NTH>
+__device__ __forceinline__ void blk_sum_rs(double (&v)[K], double* wred, double* out /* shared K */) {
+    constexpr int NW = NTH / 64, LEV = rs_levels<K>(), CNT = rs_count<K>();
+    constexpr int LOWMASK = (LEV >= 6) ? 0 : ((32 >> (LEV > 0 ? LEV - 1 : 0)) - 1) & (LEV > 0 ? 63 : 63);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    rs_halve<K, 32>(v, lane);
+    const int base = rs_base<K>(lane);
+    const int low = (LEV == 0) ? 63 : ((32 >> (LEV - 1)) - 1);
+    (void)LOWMASK;
+    if ((lane & low) == 0) {
+#pragma unroll
+        for (int j = 0; j < CNT; ++j) wred[w * K + base + j] = v[j];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double a[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) a[i] = wred[i * K + threadIdx.x];
+#pragma unroll
+        for (int st = 1; st < NW; st *= 2)
+#pragma unroll
+            for (int i = 0; i + st < NW; i += 2 * st) a[i] += a[i + st];
+        out[threadIdx.x] = a[0];
+    }
+    __syncthreads();
+}
+
+// Cross-block sum of K values per thread: block sums by reduce-scatter, k-major partials,
+// agent-scope ticket; the last block gathers the partials with 16 threads per quantity
+// (16 loads in flight each: one round trip for up to 256 blocks), pairwise throughout.
+// With 256-thread blocks and 1024 blocks the gather was 14 us of each pass; with 1024-thread
+// blocks (one per CU) and this layout of the loads it is ~3 us (tools/s2_ablation.hip).
+template <int K, int NTH>
+__device__ bool sp_reduce_last_rs(double (&v)[K], RedBuf rb, double* tot /* shared, K */) {
+    constexpr int NW = NTH / 64;
+    __shared__ double wred[NW * K];
+    __shared__ double bsum[K];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, nb = gridDim.x;
+    blk_sum_rs<K, NTH>(v, wred, bsum);
+    if (tid < K)
+        __hip_atomic_store(&rb.partials[(int64_t)tid * nb + blockIdx.x], bsum[tid], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE == 5   // timing studies only: no ticket, no tail
+    return false;
+#endif
+    if (tid < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // wave 0's stores drained before its ticket add
+        if (tid == 0) {
+            const unsigned t = __hip_atomic_fetch_add(rb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            is_last = (t == (unsigned)(nb - 1));
+        }
+    }
+    __syncthreads();
+#if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE == 6   // timing studies only: ticket, no tail
+    if (is_last && tid == 0) __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+#endif
+    if (!is_last) return false;
+    // Gather: thread t sums quantity t / 16 over the blocks b = t % 16 + 16 j (16 loads in
+    // flight per round, pairwise), then the 16 lanes of a quantity combine by xor butterfly.
+    // K * 16 threads per round of quantities (all 48 at once with 1024-thread blocks).
+    constexpr int QPR = NTH / 16;   // quantities per round
+#pragma unroll
+    for (int c = 0; c < K; c += QPR) {
+        const int k = c + (tid >> 4), sub = tid & 15;
+        double x = 0.0;
+        if (k < K) {
+            for (int base = 0; base < nb; base += 256) {
+                double y[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int b = min(base + sub + 16 * j, nb - 1);
+                    y[j] = __hip_atomic_load(&rb.partials[(int64_t)k * nb + b], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) y[j] = (base + sub + 16 * j < nb) ? y[j] : 0.0;
+#pragma unroll
+                for (int st = 1; st < 16; st *= 2)
+#pragma unroll
+                    for (int j = 0; j + st < 16; j += 2 * st) y[j] += y[j + st];
+                x += y[0];
+            }
+        }
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+        if (k < K && sub == 0) tot[k] = x;
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 constexpr int sp_chunk(int K) {   // largest divisor of K that is <= 16
     int c = K < 16 ? K : 16;
     while (K % c) --c;
@@ -1110,8 +1253,11 @@ __device__ __forceinline__ SpElem spec_elem(const SpecTab& T, int t, int ntx, in
 // gath == nullptr (FUSE): single shard, the last block plans the next pass itself.
 // Otherwise the last block stores this shard's moments at gath[rank * NACC]; after the
 // all-gather, k_spec_s2_plan sums them in rank order and plans (identically on every rank).
+// 1024 threads: one block per CU at the pass's occupancy (4 waves / SIMD), so the
+// cross-block tail gathers 48 x 256 partials in one round trip (with 256-thread blocks it
+// was 48 x 1024 in six: 14 us of each pass, tools/s2_ablation.hip).
 #ifndef FOTO_S2_NTH
-#define FOTO_S2_NTH 256
+#define FOTO_S2_NTH 1024
 #endif
 constexpr int S2_NTH = FOTO_S2_NTH;   // threads per block of the s-step pass
 
@@ -1166,6 +1312,9 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
         } else {
 #pragma unroll
             for (int i = 0; i < SMAX; ++i) {
+#if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE == 2
+                if (i >= 1) break;
+#endif
                 if (i >= ns) break;
                 // iteration k + i: p = beta p + r (p = r at k = 0); r -= alpha (lam p)
                 const double a = S0.a[i], b = S0.b[i];
@@ -1179,11 +1328,23 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
             st2<VEC>(rh, e.i, e.n2, r0, r1);
             st2<VEC>(ph, e.i, e.n2, q0, q1);
         }
+#if defined(FOTO_S2_ABLATE) && (FOTO_S2_ABLATE == 1 || FOTO_S2_ABLATE == 4)   // timing studies only
+        acc[0] += r0 * q0 + r1 * q1;
+#else
         moments(e.l0, r0, q0);
         if (e.n2 == 2) moments(e.l1, r1, q1);
+#endif
     }
     __shared__ double tot[NACC];
-    if (!sp_reduce_last_wide<NACC, S2_NTH>(acc, rb, tot)) return;
+#if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE >= 3   // timing studies only: no reduction
+    {
+        double sacc = 0.0;
+        for (int m = 0; m < NACC; ++m) sacc += acc[m];
+        if (sacc == 1.2345) gath[0] = sacc;
+        return;
+    }
+#endif
+    if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
     if (!FUSE) {
         for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
         return;
