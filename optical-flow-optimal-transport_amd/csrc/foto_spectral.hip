@@ -621,8 +621,58 @@ __device__ __forceinline__ void cmac_root(double& ar, double& ai, double xr, dou
     else if (wi != 0.0) { ar = fma(-xi, wi, ar); ai = fma(xr, wi, ai); }
 }
 
+// In-register DFT of length R (natural order in and out), mixed radix: R = R1 R2 with R1
+// the smallest of {4, 2, 3, 5} dividing R; R2 DFTs of length R1 over the stride-R2
+// subsequences, twiddles e^{-+2 pi i n2 k1 / R}, R1 DFTs of length R2 -- all indices
+// compile-time, roots folded (16 points: ~300 flops instead of 1024 FMA direct).
+template <int R>
+constexpr int dft_radix() {
+    return (R % 4 == 0 && R > 4) ? 4 : (R % 2 == 0 && R > 2) ? 2 : (R % 3 == 0 && R > 3) ? 3 : (R % 5 == 0 && R > 5) ? 5 : R;
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft_reg(double (&xr)[R], double (&xi)[R]) {
+    constexpr int R1 = dft_radix<R>();
+    if constexpr (R1 == R) {   // codelet: direct with compile-time roots
+        double yr[R], yi[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            double ar = 0.0, ai = 0.0;
+#pragma unroll
+            for (int n = 0; n < R; ++n) cmac_root<R, INV>(ar, ai, xr[n], xi[n], (n * k) % R);
+            yr[k] = ar;
+            yi[k] = ai;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) { xr[k] = yr[k]; xi[k] = yi[k]; }
+    } else {
+        constexpr int R2 = R / R1;
+        double ar[R1][R2], ai[R1][R2];   // A[k1][n2]
+#pragma unroll
+        for (int n2 = 0; n2 < R2; ++n2) {
+            double tr[R1], ti[R1];
+#pragma unroll
+            for (int n1 = 0; n1 < R1; ++n1) { tr[n1] = xr[R2 * n1 + n2]; ti[n1] = xi[R2 * n1 + n2]; }
+            dft_reg<R1, INV>(tr, ti);
+#pragma unroll
+            for (int k1 = 0; k1 < R1; ++k1) {
+                const int p = (n2 * k1) % R;
+                const double wr = root_re<R, INV>(p), wi = root_im<R, INV>(p);
+                if (p == 0) { ar[k1][n2] = tr[k1]; ai[k1][n2] = ti[k1]; }
+                else { ar[k1][n2] = fma(tr[k1], wr, -ti[k1] * wi); ai[k1][n2] = fma(tr[k1], wi, ti[k1] * wr); }
+            }
+        }
+#pragma unroll
+        for (int k1 = 0; k1 < R1; ++k1) {
+            dft_reg<R2, INV>(ar[k1], ai[k1]);
+#pragma unroll
+            for (int k2 = 0; k2 < R2; ++k2) { xr[k1 + R1 * k2] = ar[k1][k2]; xi[k1 + R1 * k2] = ai[k1][k2]; }
+        }
+    }
+}
+
 // stage 1 (in place on the LDS lines): for each (line, j2): the length-M1 DFT of
-// z[M2 j1 + j2], times e^{-+2 pi i j2 k1 / M}, stored at M2 k1 + j2
+// z[M2 j1 + j2] (dft_reg), times e^{-+2 pi i j2 k1 / M}, stored at M2 k1 + j2
 template <int M1, int M2, bool INV, int LPB>
 __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
     constexpr int M = M1 * M2, N = 2 * M;
@@ -635,15 +685,13 @@ __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
             xr[j1] = Ll[2 * (M2 * j1 + j2)];
             xi[j1] = Ll[2 * (M2 * j1 + j2) + 1];
         }
+        dft_reg<M1, INV>(xr, xi);
 #pragma unroll
         for (int k1 = 0; k1 < M1; ++k1) {
-            double ar = 0.0, ai = 0.0;
-#pragma unroll
-            for (int j1 = 0; j1 < M1; ++j1) cmac_root<M1, INV>(ar, ai, xr[j1], xi[j1], (j1 * k1) % M1);
             const int q = j2 * k1;   // < M
             const double tr = TW[2 * q], ti = INV ? -TW[2 * q + 1] : TW[2 * q + 1];
-            Ll[2 * (M2 * k1 + j2)] = fma(ar, tr, -ai * ti);
-            Ll[2 * (M2 * k1 + j2) + 1] = fma(ar, ti, ai * tr);
+            Ll[2 * (M2 * k1 + j2)] = fma(xr[k1], tr, -xi[k1] * ti);
+            Ll[2 * (M2 * k1 + j2) + 1] = fma(xr[k1], ti, xi[k1] * tr);
         }
     }
 }
@@ -662,13 +710,11 @@ __device__ __forceinline__ void fft_stage2(double* L) {
             xr[j2] = Lr[2 * j2];
             xi[j2] = Lr[2 * j2 + 1];
         }
+        dft_reg<M2, INV>(xr, xi);
 #pragma unroll
         for (int k2 = 0; k2 < M2; ++k2) {
-            double ar = 0.0, ai = 0.0;
-#pragma unroll
-            for (int j2 = 0; j2 < M2; ++j2) cmac_root<M2, INV>(ar, ai, xr[j2], xi[j2], (j2 * k2) % M2);
-            Lr[2 * k2] = ar;
-            Lr[2 * k2 + 1] = ai;
+            Lr[2 * k2] = xr[k2];
+            Lr[2 * k2 + 1] = xi[k2];
         }
     }
 }
@@ -750,7 +796,6 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB;
-    constexpr int TPT = (LPB * M + 255) / 256;   // pre-process tasks per thread
     __shared__ double L[LPB * N];
     __shared__ double TW[2 * M];
     const int tid = threadIdx.x;
@@ -760,50 +805,38 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
     };
     for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
-    for (int idx = tid; idx < LPB * N; idx += 256) {   // load X, natural order
-        int l, j;
-        if (CONTIG) { l = idx / N; j = idx - l * N; }
-        else { j = idx / LPB; l = idx - j * LPB; }
-        L[l * N + j] = (l < f.nl) ? in[base(l) + j * st] : 0.0;
-    }
-    __syncthreads();
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double is0 = 1.0 / PB[2 * (M + 1)], is = 1.0 / PB[2 * (M + 1) + 1];
-    double Zr[TPT], Zi[TPT];
-#pragma unroll
-    for (int t = 0; t < TPT; ++t) {
-        const int idx = tid + 256 * t;
-        Zr[t] = Zi[t] = 0.0;
-        if (idx >= LPB * M) continue;
-        const int l = idx / M, k = idx - (idx / M) * M;
-        const double* Ll = L + l * N;
-        // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
-        auto V = [&](int j, double& vr, double& vi) {
-            const double yr = Ll[j] * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -Ll[N - j] * is;
-            const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
-            vr = fma(wbr, yr, -wbi * yi);
-            vi = fma(wbr, yi, wbi * yr);
-        };
-        double ar, ai, br, bi;
-        V(k, ar, ai);
-        V(M - k, br, bi);
-        bi = -bi;                                                  // conj V_{M-k} = V_{k+M}
-        const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_k
-        const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
-        const double war = PA[2 * k], wai = -PA[2 * k + 1];        // e^{+2 pi i k/N}
-        const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_k
-        Zr[t] = er - oi;                                           // Z = Ve + i Vo
-        Zi[t] = ei + orr;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < TPT; ++t) {
-        const int idx = tid + 256 * t;
-        if (idx >= LPB * M) continue;
-        const int l = idx / M, k = idx - (idx / M) * M;
-        L[l * N + 2 * k] = Zr[t];
-        L[l * N + 2 * k + 1] = Zi[t];
+    // Z_k from X_k, X_{N-k}, X_{M-k}, X_{M+k}, read straight from global (L2-resident lines;
+    // no LDS image of X, so Z is written once and nothing is held in registers across a barrier)
+    for (int idx = tid; idx < LPB * M; idx += 256) {
+        int l, k;
+        if (CONTIG) { l = idx / M; k = idx - l * M; }
+        else { k = idx / LPB; l = idx - k * LPB; }
+        double zr = 0.0, zi = 0.0;
+        if (l < f.nl) {
+            const double* X = in + base(l);
+            // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
+            auto V = [&](int j, double& vr, double& vi) {
+                const double yr = X[j * st] * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -X[(N - j) * st] * is;
+                const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
+                vr = fma(wbr, yr, -wbi * yi);
+                vi = fma(wbr, yi, wbi * yr);
+            };
+            double ar, ai, br, bi;
+            V(k, ar, ai);
+            V(M - k, br, bi);
+            bi = -bi;                                                  // conj V_{M-k} = V_{k+M}
+            const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_k
+            const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
+            const double war = PA[2 * k], wai = -PA[2 * k + 1];        // e^{+2 pi i k/N}
+            const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_k
+            zr = er - oi;                                              // Z = Ve + i Vo
+            zi = ei + orr;
+        }
+        L[l * N + 2 * k] = zr;
+        L[l * N + 2 * k + 1] = zi;
     }
     __syncthreads();
     fft_stage1<M1, M2, true, LPB>(L, TW);
