@@ -153,6 +153,18 @@ int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   double rtol, int maxiter, double* u, double* v, double* m, int* iterations);
 
+/* ------------------------------------------------------------------ evaluation
+ * the warp and the error metrics of utils.py on the GPU.      */
+/* utils.apply_opticalflow(f1, u, v, w, h, m) (utils.py:186-248): backward bilinear
+ * warp of (1 + m) f1 (m may be NULL: f1 unscaled).  Bit-identical to the reference. */
+int foto_warp(const double* f1, const double* u, const double* v, const double* m, int w, int h, double* out);
+/* utils.EE and utils.AE (utils.py:294-338): out4 = {AEE, SDEE, AAE, SDAE}; EE > 50 and
+ * NaN angular errors are ignored as in the reference.                               */
+int foto_flow_errors(const double* u, const double* v, const double* uGT, const double* vGT, int w, int h,
+                     double* out4);
+/* utils.IE (utils.py:340-354): RMS of 255 I - 255 IGT.                              */
+int foto_intensity_error(const double* I, const double* IGT, int w, int h, double* ie);
+
 #ifdef __cplusplus
 }
 #endif

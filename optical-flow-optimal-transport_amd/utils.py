@@ -3,16 +3,18 @@
 Hot path (GPU, libfoto.so):
   opticalflow_from_benamoubrenier  utils.py:148-183 -> foto_flow_from_phi (one thread per
                                    pixel walks the Nt-1 trajectory steps, then m = -div_D)
-Host utilities (image / .flo IO and evaluation metrics):
-  openGrayscaleImage, reconstructTrajectory (single start point), apply_opticalflow,
-  openFlo, saveFlo, EE, AE, IE -- same semantics and quirks as utils.py:25-354
-  (vectorised over pixels instead of Python loops).
+Evaluation (GPU):
+  apply_opticalflow -> foto_warp, EE / AE -> foto_flow_errors, IE -> foto_intensity_error
+Host utilities (image and .flo IO):
+  openGrayscaleImage, reconstructTrajectory (single start point), openFlo, saveFlo --
+  same semantics and quirks as utils.py:25-292.
 """
 import math  # noqa: F401  (kept for API parity with the reference module)
 
 import numpy as np
 from PIL import Image
 
+from foto import evaluate as _ev
 from foto import ops as _ops
 
 
@@ -47,31 +49,14 @@ def opticalflow_from_benamoubrenier(phi, Nt, Nx, Ny, grad=None, div=None):
 
 
 def apply_opticalflow(f1, u, v, w, h, m=np.array([None])):
-    """Backward bilinear warp of (1+m) f1 by (u, v) with the reference's edge handling
-    (utils.py:186-248): weights from the unclamped fractional parts, indices clamped to
-    the image, the +1 neighbour collapsed onto the edge pixel on the last row / column."""
-    if m.all() != None:  # noqa: E711  -- reference quirk: true for every numeric m
-        f1 = (1 + m) * f1
-    f1 = np.asarray(f1, dtype=np.float64)
-    ii, jj = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
-    ti = ii.ravel() - np.asarray(v, dtype=np.float64)
-    tj = jj.ravel() - np.asarray(u, dtype=np.float64)
-    dI = ti - np.trunc(ti)
-    dJ = tj - np.trunc(tj)
-    w1, w2, w3, w4 = (1 - dI) * (1 - dJ), dJ * (1 - dI), dI * dJ, (1 - dJ) * dI
-    ti = np.where(ti >= h, h - 1, ti)
-    tj = np.where(tj >= w, w - 1, tj)
-    ti = np.where(ti < 0, 0, ti)
-    tj = np.where(tj < 0, 0, tj)
-    a = ti.astype(np.int64)
-    b = tj.astype(np.int64)
-    a1 = np.where(a < h - 1, a + 1, a)
-    b1 = np.where(b < w - 1, b + 1, b)
-    x = w1 * f1[a * w + b]
-    x = x + w2 * f1[a * w + b1]
-    x = x + w3 * f1[a1 * w + b1]
-    x = x + w4 * f1[a1 * w + b]
-    return x
+    """Backward bilinear warp of (1+m) f1 by (u, v) (utils.py:186-248) on the GPU
+    (foto_warp; bit-identical to the reference).  Reference behaviour kept: with numpy 2
+    ``np.array([None]).all()`` is False, so ``m.all() != None`` holds for every m and the
+    reference evaluates ``(1 + m) * f1`` -- a TypeError for the default m, as here."""
+    if m.all() != None:  # noqa: E711
+        1 + m  # noqa: B018  -- the reference's (1 + m) * f1: raises for the default np.array([None])
+        return _ev.warp(f1, u, v, w, h, m)
+    return _ev.warp(f1, u, v, w, h, None)
 
 
 def openFlo(pathname):
@@ -97,21 +82,15 @@ def saveFlo(w, h, u, v, pathname):
 
 
 def EE(w, h, u, v, uGT, vGT):
-    """Average endpoint error and its std over pixels with EE <= 50 (utils.py:294-315)."""
-    e = np.sqrt((u - uGT) ** 2 + (v - vGT) ** 2)[: w * h]
-    kept = e[e <= 50]
-    mean = np.sum(kept) / len(kept)
-    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+    """Average endpoint error and its std over pixels with EE <= 50 (utils.py:294-315), GPU."""
+    return _ev.flow_errors(u, v, uGT, vGT, w, h)[0:2]
 
 
 def AE(w, h, u, v, uGT, vGT):
-    """Average angular error (radians) and std, NaNs ignored (utils.py:317-338)."""
-    a = np.arccos((1.0 + u * uGT + v * vGT) / (np.sqrt(1.0 + u ** 2 + v ** 2) * np.sqrt(1.0 + uGT ** 2 + vGT ** 2)))
-    kept = a[: w * h][~np.isnan(a[: w * h])]
-    mean = np.sum(kept) / len(kept)
-    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+    """Average angular error (radians) and std, NaNs ignored (utils.py:317-338), GPU."""
+    return _ev.flow_errors(u, v, uGT, vGT, w, h)[2:4]
 
 
 def IE(w, h, I, IGT):
-    """RMS intensity error on the 0..255 scale (utils.py:340-354)."""
-    return np.sqrt(np.sum((255 * I - 255 * IGT) ** 2) / (w * h))
+    """RMS intensity error on the 0..255 scale (utils.py:340-354), GPU."""
+    return _ev.intensity_error(I, IGT, w, h)

@@ -387,3 +387,54 @@ def gn_solve(f1, f2, w, h, alpha, lam):
     x = spla.spsolve(A, b)
     n = w * h
     return x[:n], x[n:2 * n], x[2 * n:]
+
+
+# ----------------------------------------------------------------------------- evaluation (§8(f) row 1)
+
+def apply_opticalflow(f1, u, v, w, h, m=None):
+    """utils.apply_opticalflow (utils.py:186-248) restated over all pixels: backward
+    bilinear warp of (1+m) f1 (m None: unscaled); weights from the unclamped fractional
+    parts, indices clamped, the +1 neighbour collapsed onto the edge pixel."""
+    f1 = np.asarray(f1, dtype=np.float64)
+    if m is not None:
+        f1 = (1 + np.asarray(m, dtype=np.float64)) * f1
+    ii, jj = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
+    ti = ii.ravel() - np.asarray(v, dtype=np.float64)
+    tj = jj.ravel() - np.asarray(u, dtype=np.float64)
+    dI = ti - np.trunc(ti)
+    dJ = tj - np.trunc(tj)
+    w1, w2, w3, w4 = (1 - dI) * (1 - dJ), dJ * (1 - dI), dI * dJ, (1 - dJ) * dI
+    ti = np.where(ti >= h, h - 1, ti)
+    tj = np.where(tj >= w, w - 1, tj)
+    ti = np.where(ti < 0, 0, ti)
+    tj = np.where(tj < 0, 0, tj)
+    a = ti.astype(np.int64)
+    b = tj.astype(np.int64)
+    a1 = np.where(a < h - 1, a + 1, a)
+    b1 = np.where(b < w - 1, b + 1, b)
+    x = w1 * f1[a * w + b]
+    x = x + w2 * f1[a * w + b1]
+    x = x + w3 * f1[a1 * w + b1]
+    x = x + w4 * f1[a1 * w + b]
+    return x
+
+
+def EE(w, h, u, v, uGT, vGT):
+    """utils.EE (utils.py:294-315): mean and std of the endpoint error over EE <= 50."""
+    e = np.sqrt((u - uGT) ** 2 + (v - vGT) ** 2)[: w * h]
+    kept = e[e <= 50]
+    mean = np.sum(kept) / len(kept)
+    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+
+
+def AE(w, h, u, v, uGT, vGT):
+    """utils.AE (utils.py:317-338): mean and std of the angular error, NaN ignored."""
+    a = np.arccos((1.0 + u * uGT + v * vGT) / (np.sqrt(1.0 + u ** 2 + v ** 2) * np.sqrt(1.0 + uGT ** 2 + vGT ** 2)))
+    kept = a[: w * h][~np.isnan(a[: w * h])]
+    mean = np.sum(kept) / len(kept)
+    return mean, np.sqrt(np.sum((kept - mean) ** 2) / len(kept))
+
+
+def IE(w, h, I, IGT):
+    """utils.IE (utils.py:340-354): RMS of 255 I - 255 IGT."""
+    return np.sqrt(np.sum((255 * I - 255 * IGT) ** 2) / (w * h))

@@ -79,14 +79,41 @@ def test_flo_bytes_and_roundtrip(gold, tmp_path):
     np.testing.assert_array_equal(v2, d["v_rt"])
 
 
-def test_metrics_and_warp(gold):
+def test_metrics_and_warp_oracle(gold):
+    """The oracle's restatements of utils.EE / AE / apply_opticalflow / IE against the
+    reference's own outputs (io.npz)."""
+    from oracle import foto_oracle as O
     d = gold("io.npz")
     w, h = (int(s) for s in d["wh"])
-    np.testing.assert_allclose(U.EE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ee"], rtol=1e-14)
-    np.testing.assert_allclose(U.AE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ae"], rtol=1e-14)
+    np.testing.assert_allclose(O.EE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ee"], rtol=1e-14)
+    np.testing.assert_allclose(O.AE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ae"], rtol=1e-14)
+    rec = O.apply_opticalflow(d["f1"], d["u"], d["v"], w, h, d["m"])
+    np.testing.assert_array_equal(rec, d["rec"])
+    np.testing.assert_allclose(O.IE(w, h, np.clip(rec, 0, 1), d["f2"]), d["ie"], rtol=1e-14)
+
+
+@pytest.mark.gpu
+def test_metrics_and_warp_gpu(gold):
+    """The drop-in utils (foto_warp / foto_flow_errors / foto_intensity_error) against the
+    reference's outputs: the warp bit-identical, the metrics to summation order (1e-13)."""
+    from oracle import foto_oracle as O
+    d = gold("io.npz")
+    w, h = (int(s) for s in d["wh"])
+    np.testing.assert_allclose(U.EE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ee"], rtol=1e-13)
+    np.testing.assert_allclose(U.AE(w, h, d["u"], d["v"], d["uGT"], d["vGT"]), d["ae"], rtol=1e-13)
     rec = U.apply_opticalflow(d["f1"], d["u"], d["v"], w, h, d["m"])
     np.testing.assert_array_equal(rec, d["rec"])
-    np.testing.assert_allclose(U.IE(w, h, np.clip(rec, 0, 1), d["f2"]), d["ie"], rtol=1e-14)
+    np.testing.assert_allclose(U.IE(w, h, np.clip(rec, 0, 1), d["f2"]), d["ie"], rtol=1e-13)
+    # the default m (np.array([None])) raises like the reference (numpy 2: (1 + [None]) * f1)
+    rng = np.random.default_rng(5)
+    u, v = rng.normal(0, 4 * w, w * h), rng.normal(0, 4 * h, w * h)
+    with pytest.raises(TypeError):
+        U.apply_opticalflow(d["f1"], u, v, w, h)
+    # wild flows leave the image on every side
+    z = np.zeros(w * h)
+    np.testing.assert_array_equal(U.apply_opticalflow(d["f1"], u, v, w, h, z), O.apply_opticalflow(d["f1"], u, v, w, h, z))
+    m = rng.normal(0, 0.3, w * h)
+    np.testing.assert_array_equal(U.apply_opticalflow(d["f1"], u, v, w, h, m), O.apply_opticalflow(d["f1"], u, v, w, h, m))
 
 
 def test_reconstruct_trajectory_matches_flow(gold):
