@@ -21,6 +21,9 @@ Cases (SURVEY.md §8(c) "Golden vectors to generate"):
   gn.npz         GLLOpticalFlow assemble A@x, b, process() u, v, m on 40x30 and 17x13
   io.npz         saveFlo bytes, openFlo round trip, EE/AE/IE, apply_opticalflow
   cli.npz        main.py's pipeline on a 36x28 PNG pair (FOTO Nt=4, 8 its; GN): flows, IE, .flo bytes
+  bin.npz        the dataset-prep scripts bin/normalize_image.py, create_lum_dataset.py and
+                 data_diff.py run on a 48x40 PNG pair (decoded output pixels), and bash's
+                 RANDOM sequence after RANDOM=12345 (run.sh:33 seeds create_lum_dataset)
 """
 import argparse
 import contextlib
@@ -307,11 +310,53 @@ def gen_cli(utils, bb, classical):
     save("cli.npz", **out)
 
 
+def gen_bin(ref):
+    """run.sh's dataset-prep scripts (bin/*.py), executed as the reference runs them."""
+    import subprocess
+    from PIL import Image
+    yy, xx = np.mgrid[0:40, 0:48].astype(np.float64)
+    a = 0.5 + 0.3 * np.sin(xx / 5.0) * np.cos(yy / 7.0) + 0.1 * np.exp(-((xx - 20) ** 2 + (yy - 18) ** 2) / 60.0)
+    b = 0.5 + 0.3 * np.sin((xx - 1.5) / 5.0) * np.cos((yy - 0.5) / 7.0) + 0.1 * np.exp(-((xx - 22) ** 2 + (yy - 18) ** 2) / 60.0)
+    f1 = np.uint8(np.clip(a, 0, 1) * 255)
+    f2 = np.uint8(np.clip(b, 0, 1) * 255)
+    out = {"f1": f1, "f2": f2}
+    env = dict(os.environ, PYTHONPATH=ref)
+    with tempfile.TemporaryDirectory() as td:
+        p1, p2 = os.path.join(td, "frame10.png"), os.path.join(td, "frame11.png")
+        Image.fromarray(f1, "L").save(p1)
+        Image.fromarray(f2, "L").save(p2)
+
+        def run(script, *args):
+            subprocess.run([sys.executable, os.path.join(ref, "bin", script), *args], env=env, cwd=td, check=True)
+
+        def load(name):
+            return np.asarray(Image.open(os.path.join(td, name)).convert("L"))
+
+        run("normalize_image.py", p1, p2, "n1.png", "n2.png")
+        out["norm1"], out["norm2"] = load("n1.png"), load("n2.png")
+        run("data_diff.py", p1, p2, "diff.png")
+        out["diff"] = load("diff.png")
+        seeds = [12345, 7, 31337]
+        out["lum_seeds"] = np.array(seeds)
+        for sd in seeds:
+            run("create_lum_dataset.py", p2, f"lum{sd}.png", str(sd))
+            out[f"lum_{sd}"] = load(f"lum{sd}.png")
+    r = subprocess.run(["bash", "-c", "RANDOM=12345; for i in 1 2 3 4 5 6 7 8 9 10; do echo $RANDOM; done"],
+                       capture_output=True, text=True, check=True)
+    out["bash_random_12345"] = np.array([int(x) for x in r.stdout.split()])
+    save("bin.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--skip-c1", action="store_true")
+    ap.add_argument("--only", help="comma-separated generators to run (e.g. bin)")
     args = ap.parse_args()
+    if args.only:
+        for name in args.only.split(","):
+            {"bin": lambda: gen_bin(args.ref)}[name]()
+        return
     sys.path.insert(0, args.ref)
     import operators  # noqa: F401  (reference modules)
     import utils
@@ -329,6 +374,7 @@ def main():
     gen_cli(utils, bb, classical)
     gen_bb(bb, "bb_small.npz", 4, 20, 16, r=1, convergence_tol=0.01, reg_epsilon=1e-2, max_it=30)
     gen_bb(bb, "bb_tex.npz", 5, 24, 18, pair="tex", r=1.5, convergence_tol=0.05, reg_epsilon=1e-3, max_it=12)
+    gen_bin(args.ref)
     if not args.skip_c1:
         gen_bb(bb, "bb_c1.npz", 8, 64, 64, r=1, convergence_tol=0.01, reg_epsilon=1e-2, max_it=100)
 
