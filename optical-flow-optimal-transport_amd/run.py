@@ -1,0 +1,338 @@
+"""Drop-in for the reference's batch pipeline ``run.sh`` (run.sh:1-167), sharded over GPUs.
+
+    python run.py [download | install | prepare | restart | run] [--gpus N] [--data data] [--results results]
+
+Same data layout, same per-sequence outputs, same ``.out.gn.sucess`` / ``.out.foto.sucess``
+skip markers (run.sh:98-117, 135-154), same hyper-parameters (run.sh:103, 114):
+
+  data/middlebury-1/eval-data-gray/<seq>/frame10.png, frame11.png
+  data/middlebury-1-lum/eval-data-gray/<seq>/...          (prepare: random illumination)
+  results/<dataset>/<seq>/diff.png, {gn,foto}.flo, .benchmark.txt, .rec.png, .lum.png, .png
+
+Differences from run.sh, all deliberate:
+  * Sequences are independent jobs.  ``--gpus N`` starts N worker processes, one per GPU
+    (HIP_VISIBLE_DEVICES=i).  Worker i takes the sequences at positions i, i+N, ... of
+    the sorted (dataset, sequence) list.  Under torch.distributed.run the RANK /
+    WORLD_SIZE / LOCAL_RANK environment picks the shard instead.  No collective is
+    involved: the workers share nothing but the file system.
+  * Each worker runs main.py in-process (main.main(argv)), one HIP context per worker,
+    instead of one python3 process per solve.  Solver stdout goes to
+    results/<dataset>/<seq>/<algo>.log.
+  * The colour coding is bin/color_flow.py (the reference ships color_flow only as a
+    prebuilt binary, run.sh:104).
+  * ``prepare`` does run__resizedataset + run__createlumdataset + run__normalizedataset
+    (run.sh:18-70) on data that is already in place.  ``download`` fetches
+    eval-gray-twoframes.zip (run.sh:9-10) first; this needs network access.  The 50 %
+    resize uses PIL's Lanczos filter, not ImageMagick (run.sh:26), so resized pixels
+    can differ from magick's.  The lum seeds are bash's $RANDOM after RANDOM=12345
+    (run.sh:33), restated in bash_random(), in the same glob order.
+  * ``--dataset NAME=FRAMES_DIR[:GT_DIR]`` adds a dataset such as Middlebury-2
+    other-data-gray with other-gt-flow.  When GT_DIR/<seq>/flow10.flo exists it is passed
+    as --ground-truth, so the benchmark txt gains EE/AE.  ``results/summary.json``
+    collects every benchmark txt.
+"""
+import argparse
+import contextlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import zipfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "bin"))
+
+MIDDLEBURY_1_URL = "https://vision.middlebury.edu/flow/data/comp/zip/eval-gray-twoframes.zip"
+
+# run.sh:99-103 and run.sh:110-114
+GN_ARGS = ["--algo=GN", "--alpha=0.1", "--lambda=0.2"]
+FOTO_ARGS = ["--algo=foto", "--r=1", "--convergence-tol=0.01", "--reg-epsilon=1e-2", "--Nt=16", "--max-it=200"]
+ALGOS = (("gn", GN_ARGS), ("foto", FOTO_ARGS))
+
+
+def bash_random(seed, n):
+    """The first n values of bash's $RANDOM after RANDOM=seed (bash >= 5.1, variables.c:
+    Park-Miller minimal standard generator by Schrage's method, output
+    (x >> 16) ^ (x & 0xffff) masked to 15 bits, a value equal to the previous one is
+    redrawn).  Checked against bash itself in tests/golden/bin.npz."""
+    x, last, out = seed & 0xFFFFFFFF, 0, []
+
+    def step():
+        nonlocal x
+        s = 123459876 if x == 0 else x
+        hi, lo = divmod(s, 127773)
+        t = 16807 * lo - 2836 * hi
+        x = t + 0x7FFFFFFF if t < 0 else t
+        return ((x >> 16) ^ (x & 0xFFFF)) & 32767
+
+    for _ in range(n):
+        rv = step()
+        while rv == last:
+            rv = step()
+        last = rv
+        out.append(rv)
+    return out
+
+
+def sequences(frames_dir):
+    """The sequence directories in bash glob order (``for dir in .../*; if [ -d ]``)."""
+    if not os.path.isdir(frames_dir):
+        return []
+    return sorted(e for e in os.listdir(frames_dir) if not e.startswith(".") and os.path.isdir(os.path.join(frames_dir, e)))
+
+
+class Dataset:
+    def __init__(self, name, frames, gt=None):
+        self.name, self.frames, self.gt = name, frames, gt
+
+    def frame(self, seq, k):
+        return os.path.join(self.frames, seq, f"frame1{k}.png")
+
+    def gt_flow(self, seq):
+        if not self.gt:
+            return None
+        p = os.path.join(self.gt, seq, "flow10.flo")
+        return p if os.path.isfile(p) else None
+
+
+def datasets(args):
+    ds = [Dataset("middlebury-1", os.path.join(args.data, "middlebury-1", "eval-data-gray")),
+          Dataset("middlebury-1-lum", os.path.join(args.data, "middlebury-1-lum", "eval-data-gray"))]
+    for spec in args.dataset or []:
+        name, _, dirs = spec.partition("=")
+        frames, _, gt = dirs.partition(":")
+        if not name or not frames:
+            raise SystemExit(f"--dataset wants NAME=FRAMES_DIR[:GT_DIR], got {spec!r}")
+        ds.append(Dataset(name, frames, gt or None))
+    return ds
+
+
+# ---------------------------------------------------------------- data preparation (run.sh:3-70)
+
+def resize_dataset(ds):
+    """run__resizedataset (run.sh:18-30): both frames halved in place."""
+    from PIL import Image
+    print("Resizing datasets")
+    for seq in sequences(ds.frames):
+        for k in (0, 1):
+            p = ds.frame(seq, k)
+            im = Image.open(p)
+            im.resize((max(1, round(im.width * 0.5)), max(1, round(im.height * 0.5))), Image.LANCZOS).save(p)
+
+
+def create_lum_dataset(src, dst, seed=12345):
+    """run__createlumdataset (run.sh:32-48): frame10 copied, frame11 with random
+    illumination seeded by successive bash $RANDOM values."""
+    from _common import open_gray, save_gray
+    from create_lum_dataset import lum_image
+    print("Adding random artifical illumination")
+    seqs = sequences(src.frames)
+    os.makedirs(dst.frames, exist_ok=True)
+    for seq, sd in zip(seqs, bash_random(seed, len(seqs))):
+        os.makedirs(os.path.join(dst.frames, seq), exist_ok=True)
+        shutil.copyfile(src.frame(seq, 0), dst.frame(seq, 0))
+        f, w, h = open_gray(src.frame(seq, 1))
+        save_gray(lum_image(f, w, h, sd), w, h, dst.frame(seq, 1))
+
+
+def normalize_dataset(ds):
+    """run__normalizedataset (run.sh:50-70): bin/normalize_image.py in place."""
+    from _common import open_gray, save_gray
+    from normalize_image import normalize_pair
+    for seq in sequences(ds.frames):
+        f1, w, h = open_gray(ds.frame(seq, 0))
+        f2, w, h = open_gray(ds.frame(seq, 1))
+        f1, f2 = normalize_pair(f1, f2)
+        save_gray(f1, w, h, ds.frame(seq, 0))
+        save_gray(f2, w, h, ds.frame(seq, 1))
+
+
+def prepare(args):
+    m1, lum = datasets(args)[:2]
+    if not sequences(m1.frames):
+        raise SystemExit(f"no sequences under {m1.frames}: unpack eval-gray-twoframes.zip there first (or `run.py download`)")
+    resize_dataset(m1)
+    create_lum_dataset(m1, lum)
+    print("Normalizing datasets")
+    normalize_dataset(m1)
+    normalize_dataset(lum)
+
+
+def download(args):
+    """run__download (run.sh:3-16)."""
+    import urllib.request
+    shutil.rmtree(args.data, ignore_errors=True)
+    os.makedirs(args.data)
+    zpath = os.path.join(args.data, "eval-gray-twoframes.zip")
+    try:
+        urllib.request.urlretrieve(MIDDLEBURY_1_URL, zpath)
+    except OSError as e:
+        raise SystemExit(f"download of {MIDDLEBURY_1_URL} failed ({e}); place the sequences under "
+                         f"{os.path.join(args.data, 'middlebury-1', 'eval-data-gray')} and run `run.py prepare`")
+    with zipfile.ZipFile(zpath) as z:
+        z.extractall(os.path.join(args.data, "middlebury-1"), [n for n in z.namelist() if n.startswith("eval-data-gray/")])
+    os.remove(zpath)
+    prepare(args)
+
+
+# ---------------------------------------------------------------- the run loop (run.sh:81-157)
+
+def jobs(args):
+    """Every (dataset, sequence) pair, in run.sh's order."""
+    return [(ds, seq) for ds in datasets(args) for seq in sequences(ds.frames)]
+
+
+def shard(items, rank, world):
+    return items[rank::world]
+
+
+def run_main(argv, log_path):
+    """main.py in-process, its stdout captured to log_path."""
+    import main as cli
+    with open(log_path, "w") as log, contextlib.redirect_stdout(log):
+        cli.main(argv)
+
+
+def color_flow(flo, png):
+    from PIL import Image
+    import utils
+    from color_flow import flow_to_color
+    w, h, u, v = utils.openFlo(flo)
+    Image.fromarray(flow_to_color(u, v, w, h), "RGB").save(png)
+
+
+def run_sequence(ds, seq, results, device=-1, extra=()):
+    """One sequence: diff, then GN and FOTO unless their markers exist (run.sh:86-118)."""
+    from _common import open_gray, save_gray
+    from data_diff import frame_diff
+    out = os.path.join(results, ds.name, seq)
+    os.makedirs(out, exist_ok=True)
+    f0, f1 = ds.frame(seq, 0), ds.frame(seq, 1)
+    a, w, h = open_gray(f0)
+    b, w, h = open_gray(f1)
+    save_gray(frame_diff(a, b), w, h, os.path.join(out, "diff.png"))
+    done = []
+    gt = ds.gt_flow(seq)
+    for algo, algo_args in ALGOS:
+        marker = os.path.join(out, f".out.{algo}.sucess")
+        if os.path.isfile(marker):
+            continue
+        p = lambda suffix: os.path.join(out, f"{algo}.{suffix}")  # noqa: E731
+        argv = [f0, f1, f"--out={p('flo')}", f"--save-benchmark={p('benchmark.txt')}",
+                f"--save-reconstruction={p('rec.png')}", f"--save-lum={p('lum.png')}", *algo_args,
+                f"--device={device}", *extra]
+        if gt:
+            argv.append(f"--ground-truth={gt}")
+        run_main(argv, p("log"))
+        color_flow(p("flo"), p("png"))
+        open(marker, "w").close()
+        done.append(algo)
+    return done
+
+
+def read_benchmark(path):
+    vals = {}
+    with open(path) as f:
+        for line in f:
+            k, _, v = line.partition(":")
+            vals[k.strip()] = float(v.strip().rstrip("s"))
+    return vals
+
+
+def summarize(args):
+    rows = []
+    for ds, seq in jobs(args):
+        for algo, _ in ALGOS:
+            p = os.path.join(args.results, ds.name, seq, f"{algo}.benchmark.txt")
+            if os.path.isfile(p):
+                rows.append({"dataset": ds.name, "sequence": seq, "algo": algo, **read_benchmark(p)})
+    with open(os.path.join(args.results, "summary.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    return rows
+
+
+def worker(args, rank, world, device):
+    mine = shard(jobs(args), rank, world)
+    for ds, seq in mine:
+        done = run_sequence(ds, seq, args.results, device, args.extra)
+        print(f"[rank {rank}/{world}] {ds.name}/{seq}: " + (", ".join(done) if done else "skipped (markers present)"),
+              flush=True)
+    return 0
+
+
+def run(args):
+    os.makedirs(args.results, exist_ok=True)
+    if "WORLD_SIZE" in os.environ:       # launched one process per GPU by torch.distributed.run
+        rank, world = int(os.environ.get("RANK", 0)), int(os.environ["WORLD_SIZE"])
+        rc = worker(args, rank, world, int(os.environ.get("LOCAL_RANK", 0)))
+        if rank == 0:
+            summarize(args)
+        return rc
+    if args.worker_rank is not None:
+        return worker(args, args.worker_rank, args.gpus, -1)
+    if args.gpus <= 1:
+        rc = worker(args, 0, 1, -1)
+    else:
+        # one child per GPU; this process never touches the device
+        procs = []
+        for i in range(args.gpus):
+            env = dict(os.environ, HIP_VISIBLE_DEVICES=str(i))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "run", f"--gpus={args.gpus}",
+                                           f"--worker-rank={i}", *forward_args(args)], env=env))
+        rc = max(p.wait() for p in procs)
+    summarize(args)
+    return rc
+
+
+def forward_args(args):
+    out = [f"--data={args.data}", f"--results={args.results}"]
+    out += [f"--dataset={d}" for d in args.dataset or []]
+    if args.extra:
+        out += ["--", *args.extra]
+    return out
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="batch pipeline (run.sh)")
+    p.add_argument("command", nargs="?", default="run", choices=["download", "install", "prepare", "restart", "run"])
+    p.add_argument("--gpus", type=int, default=1, help="worker processes, one per GPU")
+    p.add_argument("--data", default="data")
+    p.add_argument("--results", default="results")
+    p.add_argument("--dataset", action="append", help="extra dataset NAME=FRAMES_DIR[:GT_DIR]")
+    p.add_argument("--worker-rank", type=int, default=None, help=argparse.SUPPRESS)
+    return p
+
+
+def parse_args(argv=None):
+    """run.py's options; everything after `--` is passed to every main.py solve
+    (e.g. `-- --cg-mode=2`)."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    extra = []
+    if "--" in argv:
+        i = argv.index("--")
+        argv, extra = argv[:i], argv[i + 1:]
+    args = build_parser().parse_args(argv)
+    args.extra = extra
+    return args
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.command == "download":
+        download(args)
+        return 0
+    if args.command == "install":
+        print("nothing to install: numpy, scipy and Pillow plus libfoto.so (make -C csrc)")
+        return 0
+    if args.command == "prepare":
+        prepare(args)
+        return 0
+    if args.command == "restart":
+        shutil.rmtree(args.results, ignore_errors=True)
+    return run(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
