@@ -590,19 +590,28 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 // Per-axis table (fp64): WM[2M] = e^{-2 pi i p/M}, PA[2(M+1)] = e^{-2 pi i k/N},
 // PB[2(M+1)] = e^{-i pi k/(2N)}, then s_0, s.
 
+// LDS image of a line: complex element j (natural order, index M2 j1 + j2) at position
+// j1 (M2 + 1) + j2 -- each M2-row padded by one complex, so stage 2 (one thread per row,
+// lane stride M2 + 1 complex) is free of bank conflicts (unpadded, the stride is 2 M2
+// doubles: 32-way conflicts at M2 = 16), while stage 1 still touches only its own
+// positions (. (M2 + 1) + j2) and runs in place.
 template <int M1, int M2>
 struct FftGeom {
     static constexpr int M = M1 * M2, N = 2 * M;
+    static constexpr int LS = 2 * M1 * (M2 + 1);   // doubles per line in LDS
     // lines per block: LDS (lines + twiddles) <= 64 KB
     static constexpr int lpb() {
         const int c[8] = {64, 32, 16, 12, 8, 4, 2, 1};
         for (int i = 0; i < 8; ++i)
-            if (c[i] * N * 8 + 16 * M <= 65536) return c[i];
+            if (c[i] * LS * 8 + 16 * M <= 65536) return c[i];
         return 1;
     }
     static constexpr int LPB = lpb();
     static constexpr int TAB = 6 * M + 6;
 };
+
+template <int M2>
+__device__ __forceinline__ int fft_zpos(int j) { return j + j / M2; }   // natural index -> LDS complex position
 
 template <int R, bool INV>
 __device__ __forceinline__ constexpr double root_re(int p) { return Roots<R>::re[p]; }
@@ -672,38 +681,38 @@ __device__ __forceinline__ void dft_reg(double (&xr)[R], double (&xi)[R]) {
 }
 
 // stage 1 (in place on the LDS lines): for each (line, j2): the length-M1 DFT of
-// z[M2 j1 + j2] (dft_reg), times e^{-+2 pi i j2 k1 / M}, stored at M2 k1 + j2
+// z[M2 j1 + j2] (dft_reg), times e^{-+2 pi i j2 k1 / M}, stored at row k1, column j2
 template <int M1, int M2, bool INV, int LPB>
 __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
-    constexpr int M = M1 * M2, N = 2 * M;
+    constexpr int LS = FftGeom<M1, M2>::LS;
     for (int task = threadIdx.x; task < LPB * M2; task += 256) {
         const int l = task / M2, j2 = task - (task / M2) * M2;
-        double* Ll = L + l * N;
+        double* Ll = L + l * LS;
         double xr[M1], xi[M1];
 #pragma unroll
         for (int j1 = 0; j1 < M1; ++j1) {
-            xr[j1] = Ll[2 * (M2 * j1 + j2)];
-            xi[j1] = Ll[2 * (M2 * j1 + j2) + 1];
+            xr[j1] = Ll[2 * ((M2 + 1) * j1 + j2)];
+            xi[j1] = Ll[2 * ((M2 + 1) * j1 + j2) + 1];
         }
         dft_reg<M1, INV>(xr, xi);
 #pragma unroll
         for (int k1 = 0; k1 < M1; ++k1) {
             const int q = j2 * k1;   // < M
             const double tr = TW[2 * q], ti = INV ? -TW[2 * q + 1] : TW[2 * q + 1];
-            Ll[2 * (M2 * k1 + j2)] = fma(xr[k1], tr, -xi[k1] * ti);
-            Ll[2 * (M2 * k1 + j2) + 1] = fma(xr[k1], ti, xi[k1] * tr);
+            Ll[2 * ((M2 + 1) * k1 + j2)] = fma(xr[k1], tr, -xi[k1] * ti);
+            Ll[2 * ((M2 + 1) * k1 + j2) + 1] = fma(xr[k1], ti, xi[k1] * tr);
         }
     }
 }
 
-// stage 2 (in place): for each (line, k1): the length-M2 DFT of the row M2 k1 + j2; element
-// k = k1 + M1 k2 of the result lands at position M2 k1 + k2
+// stage 2 (in place): for each (line, k1): the length-M2 DFT of row k1; element
+// k = k1 + M1 k2 of the result lands at row k1, column k2
 template <int M1, int M2, bool INV, int LPB>
 __device__ __forceinline__ void fft_stage2(double* L) {
-    constexpr int M = M1 * M2, N = 2 * M;
+    constexpr int LS = FftGeom<M1, M2>::LS;
     for (int task = threadIdx.x; task < LPB * M1; task += 256) {
         const int l = task / M1, k1 = task - (task / M1) * M1;
-        double* Lr = L + l * N + 2 * M2 * k1;
+        double* Lr = L + l * LS + 2 * (M2 + 1) * k1;
         double xr[M2], xi[M2];
 #pragma unroll
         for (int j2 = 0; j2 < M2; ++j2) {
@@ -720,7 +729,7 @@ __device__ __forceinline__ void fft_stage2(double* L) {
 }
 
 template <int M1, int M2>
-__device__ __forceinline__ int fft_pos(int k) { return M2 * (k % M1) + k / M1; }   // where Z_k lands
+__device__ __forceinline__ int fft_pos(int k) { return (M2 + 1) * (k % M1) + k / M1; }   // where Z_k lands
 
 struct FftLines {   // this block's lines: CONTIG rows o0 + l, or columns (o0, i0 + l) of stride `inner`
     int o0, i0, nl;
@@ -746,8 +755,8 @@ template <int M1, int M2, bool CONTIG>
 __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2>;
-    constexpr int M = G::M, N = G::N, LPB = G::LPB;
-    __shared__ double L[LPB * N];
+    constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
+    __shared__ double L[LPB * LS];
     __shared__ double TW[2 * M];
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
@@ -761,7 +770,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
         if (CONTIG) { l = idx / N; j = idx - l * N; }
         else { j = idx / LPB; l = idx - j * LPB; }
         const double x = (l < f.nl) ? in[base(l) + j * st] : 0.0;
-        L[l * N + ((j & 1) ? N - 1 - (j >> 1) : (j >> 1))] = x;
+        const int p = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+        L[l * LS + 2 * fft_zpos<M2>(p >> 1) + (p & 1)] = x;
     }
     __syncthreads();
     fft_stage1<M1, M2, false, LPB>(L, TW);
@@ -776,7 +786,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
         if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
         else { k = idx / LPB; l = idx - k * LPB; }
         if (l >= f.nl) continue;
-        const double* Ll = L + l * N;
+        const double* Ll = L + l * LS;
         const int pa = 2 * fft_pos<M1, M2>(k == M ? 0 : k), pb = 2 * fft_pos<M1, M2>(k == 0 ? 0 : M - k);
         const double zr = Ll[pa], zi = Ll[pa + 1], cr = Ll[pb], ci = -Ll[pb + 1];
         const double er = 0.5 * (zr + cr), ei = 0.5 * (zi + ci);     // DFT of the even samples
@@ -795,8 +805,8 @@ template <int M1, int M2, bool CONTIG>
 __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2>;
-    constexpr int M = G::M, N = G::N, LPB = G::LPB;
-    __shared__ double L[LPB * N];
+    constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
+    __shared__ double L[LPB * LS];
     __shared__ double TW[2 * M];
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
@@ -835,8 +845,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
             zr = er - oi;                                              // Z = Ve + i Vo
             zi = ei + orr;
         }
-        L[l * N + 2 * k] = zr;
-        L[l * N + 2 * k + 1] = zi;
+        L[l * LS + 2 * fft_zpos<M2>(k)] = zr;
+        L[l * LS + 2 * fft_zpos<M2>(k) + 1] = zi;
     }
     __syncthreads();
     fft_stage1<M1, M2, true, LPB>(L, TW);
@@ -850,7 +860,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
         else { i = idx / LPB; l = idx - i * LPB; }
         if (l >= f.nl) continue;
         const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
-        out[base(l) + i * st] = L[l * N + 2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
+        out[base(l) + i * st] = L[l * LS + 2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
     }
 }
 
@@ -1305,7 +1315,8 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
     const double c0 = S0.c0, ic1 = 1.0 / S0.c1;
     const bool loadq = !INIT && k > 0;
-    const double* src = INIT ? bh : rh;
+    // r_0 = b^: the INIT pass (or the fused t-axis kernel, which writes no r^) leaves it in b^
+    const double* src = (INIT || k == 0) ? bh : rh;
     double acc[NACC];
 #pragma unroll
     for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
@@ -1369,7 +1380,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
 #endif
     }
     __shared__ double tot[NACC];
-#if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE >= 3   // timing studies only: no reduction
+#if defined(FOTO_S2_ABLATE) && (FOTO_S2_ABLATE == 3 || FOTO_S2_ABLATE == 4)   // timing studies only: no reduction
     {
         double sacc = 0.0;
         for (int m = 0; m < NACC; ++m) sacc += acc[m];
@@ -1401,6 +1412,129 @@ __global__ __launch_bounds__(64) void k_spec_s2_plan(SStep* Sg, const double* __
     if (!init && S0.done) return;
     __shared__ double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, init, rtol, maxiter);
+}
+
+// ============================================================================ t axis, one thread per column
+//
+// The t-axis DCT of a single shard's spectral box [kt][ky][kx]: ncols = Ny Nx columns of NTT
+// values at stride ncols.  A thread holds its column in registers, folds it into even / odd
+// halves (C[k][NTT-1-j] = (-1)^k C[k][j]) and applies the two NTT/2 x NTT/2 halves of the
+// DCT-II matrix, whose entries are wave-uniform (scalar loads): NTT^2 / 2 FMA per column and
+// one read + one write of the volume, coalesced across the threads of a wave.  Ch holds
+// E[m][j] = C[2m][j], then O[m][j] = C[2m+1][j] (m, j < NTT/2).  Two fusions remove whole
+// passes from the s-step solve:
+//   forward (+ INIT): b^ and, in the same sweep, the Chebyshev moments of r_0 = b^ (q = 0;
+//     k_spec_s2<INIT>'s per-element formula), summed across blocks; the last block plans
+//     the first pass.  The first pass reads r_0 from b^, so no r^ = b^ copy is made.
+//   inverse (+ xhat): x^ = (b^ - r^) / lam formed in registers from b^ and r^.
+template <int NTT>
+struct TCol {
+    static constexpr int H = NTT / 2;
+    static_assert(NTT % 2 == 0 && NTT >= 2 && NTT <= 32, "even column lengths up to 32");
+};
+
+constexpr int TC_NTH = 256;
+
+template <int NTT>
+__global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const double* __restrict__ Ch,
+                                                           const double* __restrict__ in, double* __restrict__ bh,
+                                                           SStep* Sg, RedBuf rb, double rtol, int maxiter) {
+    constexpr int H = TCol<NTT>::H;
+    const int64_t ncols = (int64_t)T.nyl * T.Nx;
+    const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
+    const SStep S0 = *Sg;
+    const double c0 = S0.c0, ic1 = 1.0 / S0.c1;
+    double acc[NMOM];
+#pragma unroll
+    for (int m = 0; m < NMOM; ++m) acc[m] = 0.0;
+    if (c < ncols) {
+        const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
+        double s[H], d[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const double a = in[j * ncols + c], b = in[(NTT - 1 - j) * ncols + c];
+            s[j] = a + b;
+            d[j] = a - b;
+        }
+        auto emit = [&](int k, double X) {
+            bh[k * ncols + c] = X;
+            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+            const double x = (lam - c0) * ic1, x2 = x + x, rr = X * X;
+            acc[0] += rr;
+            acc[1] = fma(x, rr, acc[1]);
+            double tm2 = 1.0, tm1 = x;
+#pragma unroll
+            for (int m = 2; m < NMOM; ++m) {
+                const double t = fma(x2, tm1, -tm2);
+                acc[m] = fma(t, rr, acc[m]);
+                tm2 = tm1;
+                tm1 = t;
+            }
+        };
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            double e = 0.0, o = 0.0;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                e = fma(Ch[m * H + j], s[j], e);
+                o = fma(Ch[H * H + m * H + j], d[j], o);
+            }
+            emit(2 * m, e);
+            emit(2 * m + 1, o);
+        }
+    }
+    __shared__ double tot[NACC];
+    if (!sp_reduce_last_rs<NMOM, TC_NTH>(acc, rb, tot)) return;
+    for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    __shared__ double xb[3 * NG + 2];
+    sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
+}
+
+// Sg->k = iterations applied; 0: no pass ran, r^ was never written and r = b^ (x^ = 0)
+template <int NTT>
+__global__ __launch_bounds__(TC_NTH) void k_dct_t_inv_xhat(SpecTab T, const double* __restrict__ Ch,
+                                                           const double* __restrict__ bh, const double* __restrict__ rh,
+                                                           const SStep* Sg, double* __restrict__ out) {
+    constexpr int H = TCol<NTT>::H;
+    const int64_t ncols = (int64_t)T.nyl * T.Nx;
+    const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
+    if (c >= ncols) return;
+    if (Sg->k == 0) rh = bh;
+    const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
+    double xe[H], xo[H];   // x^_{2m}, x^_{2m+1}
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int k = 2 * m + p;
+            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+            const double v = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+            if (p == 0) xe[m] = v;
+            else xo[m] = v;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        double e = 0.0, o = 0.0;
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            e = fma(Ch[m * H + j], xe[m], e);
+            o = fma(Ch[H * H + m * H + j], xo[m], o);
+        }
+        out[j * ncols + c] = e + o;
+        out[(NTT - 1 - j) * ncols + c] = e - o;
+    }
+}
+
+#define FOTO_TCOL_SIZES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(32)
+
+static bool tcol_supported(int n) {
+#define FOTO_TCOL_CASE(NN) if (n == NN) return true;
+    FOTO_TCOL_SIZES(FOTO_TCOL_CASE)
+#undef FOTO_TCOL_CASE
+    return false;
 }
 
 // balanced contiguous split of n items over W parts (csrc/foto_bb.cpp split_planes)
@@ -1456,6 +1590,9 @@ struct SpecImpl {
     SStep* S2 = nullptr;
     SStep* hS2 = nullptr;
     int nblocks2 = 0;
+    double* Cth = nullptr;        // t-axis DCT-II even | odd halves (column kernels)
+    bool tcol = false;            // single shard, s-step, Nt in FOTO_TCOL_SIZES
+    int tcol_nb = 0;              // column kernels' blocks
     int last_passes = 0;          // passes of the previous s-step solve (first chunk size)
     int sstep = 1;
     bool split_plan = false;
@@ -1592,7 +1729,25 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         const int want = e ? std::max(1, atoi(e)) : std::max(1, per_cu) * cus;
         P->nblocks2 = std::min(ntiles2, want);
     }
-    const int cap = std::max(2 * P->nblocks, NACC * P->nblocks2);
+    {
+        const char* e = getenv("FOTO_TCOL");   // 0: t axis by dct_pass + separate INIT / xhat passes (A/B runs)
+        P->tcol = world == 1 && sstep == 2 && tcol_supported(g.Nt) && !(e && atoi(e) == 0);
+    }
+    if (P->tcol) {
+        const int H = g.Nt / 2;
+        dct_matrix(g.Nt, C, CT, mu);
+        std::vector<double> ch((size_t)2 * H * H);
+        for (int m = 0; m < H; ++m)
+            for (int j = 0; j < H; ++j) {
+                ch[(size_t)m * H + j] = C[(size_t)(2 * m) * g.Nt + j];
+                ch[(size_t)H * H + m * H + j] = C[(size_t)(2 * m + 1) * g.Nt + j];
+            }
+        FOTO_TRY(P->alloc(ch.size() * 8, &b));
+        P->Cth = (double*)b;
+        FOTO_HIP_CHECK(hipMemcpy(P->Cth, ch.data(), ch.size() * 8, hipMemcpyHostToDevice));
+        P->tcol_nb = (int)(((int64_t)P->nyl * g.Nx + TC_NTH - 1) / TC_NTH);
+    }
+    const int cap = std::max({2 * P->nblocks, NACC * P->nblocks2, NMOM * P->tcol_nb});
     FOTO_TRY(P->alloc(sizeof(double) * (cap + 8), &b));
     P->rb.partials = (double*)b;
     P->rb.ticket = (unsigned*)((double*)b + cap);
@@ -1678,11 +1833,12 @@ static int reset_s2(SpecImpl* P, hipStream_t s) {
     return 0;
 }
 
+// init_done: the fused t-axis kernel already reset the state, took r_0's moments and planned
 static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* iters, int* info, KTimer* kt,
-                    hipStream_t s) {
+                    hipStream_t s, bool init_done = false) {
     const double N = P->nbox();
-    FOTO_TRY(reset_s2(P, s));
-    {
+    if (!init_done) {
+        FOTO_TRY(reset_s2(P, s));
         hipEvent_t e = kt ? kt->start(s) : nullptr;
         FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, nullptr, s));
         if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * N);
@@ -1726,6 +1882,42 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
     return hipGetLastError();
 }
 
+static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* out, double rtol, int maxiter,
+                              hipStream_t s) {
+    const SpecTab T = P->tab();
+    const int nb = P->tcol_nb;
+#define FOTO_TCOL_LAUNCH(NN)                                                                                       \
+    if (P->g.Nt == NN) {                                                                                           \
+        if (inv) k_dct_t_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);                  \
+        else k_dct_t_fwd_init<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter);        \
+        return hipGetLastError();                                                                                  \
+    }
+    FOTO_TCOL_SIZES(FOTO_TCOL_LAUNCH)
+#undef FOTO_TCOL_LAUNCH
+    return hipErrorNotSupported;
+}
+
+// single shard, s-step, column-kernel t axis: b -x-> tmp -y-> b -t(+INIT)-> b^; CG passes;
+// (b^, r^) -t(+xhat)-> b -y-> tmp -x-> x
+static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxiter, int predicted, int* iters,
+                      int* info, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    FOTO_TRY(reset_s2(P, s));
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, b, s));
+    FOTO_HIP_CHECK(launch_tcol(P, false, b, nullptr, rtol, maxiter, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    FOTO_TRY(solve_s2(P, rtol, maxiter, predicted, iters, info, kt, s, true));
+    e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, b, rtol, maxiter, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, b, P->tmp, s));
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, P->tmp, x, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 7.0 * 8.0 * N);
+    return 0;
+}
+
 int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info,
                         KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
@@ -1733,6 +1925,7 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     const SpecTab T = P->tab();
     const double N = (double)g.Nt * (double)g.nxy;
     const bool vec = P->vec();
+    if (P->tcol) return solve_tcol(P, b, x, rtol, maxiter, predicted, iters, info, kt, s);
     // b (physical) -> b^ ; b is scratch afterwards
     FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
     if (P->sstep == 2) {

@@ -104,9 +104,17 @@ def test_cg(gold, mode):
         np.testing.assert_allclose(x5, d[f"c{c}_x_max5"], rtol=0, atol=1e-10 * np.abs(d[f"c{c}_x_max5"]).max())
 
 
-def test_cg_zero_rhs():
-    x, info, its = ops.cg(np.zeros(4 * 5 * 6), 4, 6, 5, 1.0, 1e-2)
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("Nt", [4, 5])   # mode 2: Nt = 4 takes the fused t-axis column kernels, 5 the GEMM path
+def test_cg_zero_iterations(mode, Nt):
+    """No CG iteration runs (b = 0, or maxiter = 0): x = x0 = 0 exactly, as scipy returns."""
+    Ny, Nx = 6, 5
+    x, info, its = ops.cg(np.zeros(Nt * Ny * Nx), Nt, Nx, Ny, 1.0, 1e-2, mode=mode)
     assert info == 0 and its == 0 and not np.any(x)
+    b = np.random.default_rng(Nt).standard_normal(Nt * Ny * Nx)
+    x, info, its = ops.cg(b, Nt, Nx, Ny, 1.0, 1e-2, 1e-6, 0, mode)
+    xo, info_o, its_o = O.cg(lambda v: O.apply_A(v, 1.0, 1e-2, Nt, Ny, Nx), b, 1e-6, 0)
+    assert (info, its) == (info_o, its_o) and not np.any(x) and not np.any(xo)
 
 
 def test_bb_step_cg(gold):

@@ -22,13 +22,17 @@ import json
 import os
 
 SHORT = {
-    "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox": "prox", "k_rhs": "rhs", "k_spec": "spec_cg",
-    "k_dct": "dct", "k_traj": "flow", "k_gn_pcg_dir": "gn_dir", "k_gn_pcg_upd": "gn_upd",
+    # first match wins: the specific names before their prefixes
+    "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox": "prox", "k_rhs": "rhs",
+    "k_spec_s2_plan": "spec_plan", "k_spec_s2": "spec_cg", "k_spec_init": "spec_init", "k_spec_xhat": "spec_xhat",
+    "k_spec_cg": "spec_cg1", "k_dct_fft": "dct_fft", "k_dct": "dct_gemm", "k_traj": "flow",
+    "k_gn_pcg_dir": "gn_dir", "k_gn_pcg_upd": "gn_upd",
 }
 
 
 # bytes per lane of each hot kernel's streaming loads (csrc/*.hip)
-LOAD_WIDTH = {"spec_cg": 16, "cg_upd": 8, "cg_dir": 8, "prox": 8, "rhs": 8, "dct": 8, "flow": 8,
+LOAD_WIDTH = {"spec_cg": 16, "spec_cg1": 16, "spec_init": 16, "spec_xhat": 16, "cg_upd": 8, "cg_dir": 8, "prox": 8,
+              "rhs": 8, "dct_fft": 8, "dct_gemm": 8, "flow": 8,
               "gn_dir": 8, "gn_upd": 8}
 CALIB_BYTES = {"rd8": 2 << 30, "rd16": 2 << 30, "wr8": 1 << 30, "wr16": 1 << 30}
 
