@@ -595,6 +595,15 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 // lane stride M2 + 1 complex) is free of bank conflicts (unpadded, the stride is 2 M2
 // doubles: 32-way conflicts at M2 = 16), while stage 1 still touches only its own
 // positions (. (M2 + 1) + j2) and runs in place.
+#ifndef FOTO_FFT_TW_LDS
+#define FOTO_FFT_TW_LDS 0      // 1: stage-1 twiddles staged in LDS (costs lines per block; measured slower)
+#endif
+#ifndef FOTO_FFT_LPB_MAX
+#define FOTO_FFT_LPB_MAX 64
+#endif
+#ifndef FOTO_FFT_LPB_POW2
+#define FOTO_FFT_LPB_POW2 1    // power-of-two line counts only (whole 128-B segments on strided axes)
+#endif
 template <int M1, int M2>
 struct FftGeom {
     static constexpr int M = M1 * M2, N = 2 * M;
@@ -603,7 +612,9 @@ struct FftGeom {
     static constexpr int lpb() {
         const int c[8] = {64, 32, 16, 12, 8, 4, 2, 1};
         for (int i = 0; i < 8; ++i)
-            if (c[i] * LS * 8 + 16 * M <= 65536) return c[i];
+            if (c[i] <= FOTO_FFT_LPB_MAX && !(FOTO_FFT_LPB_POW2 && c[i] == 12) &&
+                c[i] * LS * 8 + (FOTO_FFT_TW_LDS ? 16 * M : 0) <= 65536)
+                return c[i];
         return 1;
     }
     static constexpr int LPB = lpb();
@@ -751,27 +762,56 @@ __device__ __forceinline__ FftLines fft_lines(int outer, int inner) {
     return f;
 }
 
+// Phase loops run a compile-time number of rounds over idx = tid + 256 j (predicated), so a
+// thread's global loads are all issued before the first is consumed: a tid-strided runtime
+// loop compiled to load -> wait -> LDS store per element, one load in flight per thread.
+template <int COUNT>
+struct FftRounds {
+    static constexpr int R = (COUNT + 255) / 256;
+    static __device__ __forceinline__ bool ok(int idx) { return COUNT % 256 == 0 || idx < COUNT; }
+};
+
 template <int M1, int M2, bool CONTIG>
 __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
+#if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
+#else
+    const double* TW = tab;
+#endif
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
     };
+#if FOTO_FFT_TW_LDS
     for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
-    for (int idx = tid; idx < LPB * N; idx += 256) {   // load, Makhoul order
-        int l, j;
-        if (CONTIG) { l = idx / N; j = idx - l * N; }
-        else { j = idx / LPB; l = idx - j * LPB; }
-        const double x = (l < f.nl) ? in[base(l) + j * st] : 0.0;
-        const int p = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
-        L[l * LS + 2 * fft_zpos<M2>(p >> 1) + (p & 1)] = x;
+#endif
+    {   // load (all rounds' loads in flight), then store in Makhoul order
+        using RD = FftRounds<LPB * N>;
+        double xv[RD::R];
+#pragma unroll
+        for (int j0 = 0; j0 < RD::R; ++j0) {
+            const int idx = tid + 256 * j0;
+            int l, j;
+            if (CONTIG) { l = idx / N; j = idx - l * N; }
+            else { j = idx / LPB; l = idx - j * LPB; }
+            xv[j0] = (RD::ok(idx) && l < f.nl) ? in[base(l) + j * st] : 0.0;
+        }
+#pragma unroll
+        for (int j0 = 0; j0 < RD::R; ++j0) {
+            const int idx = tid + 256 * j0;
+            if (!RD::ok(idx)) continue;
+            int l, j;
+            if (CONTIG) { l = idx / N; j = idx - l * N; }
+            else { j = idx / LPB; l = idx - j * LPB; }
+            const int p = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+            L[l * LS + 2 * fft_zpos<M2>(p >> 1) + (p & 1)] = xv[j0];
+        }
     }
     __syncthreads();
     fft_stage1<M1, M2, false, LPB>(L, TW);
@@ -781,7 +821,11 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double s0 = PB[2 * (M + 1)], s = PB[2 * (M + 1) + 1];
-    for (int idx = tid; idx < LPB * (M + 1); idx += 256) {
+    using RO = FftRounds<LPB * (M + 1)>;
+#pragma unroll
+    for (int j0 = 0; j0 < RO::R; ++j0) {
+        const int idx = tid + 256 * j0;
+        if (!RO::ok(idx)) continue;
         int l, k;
         if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
         else { k = idx / LPB; l = idx - k * LPB; }
@@ -807,36 +851,61 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     using G = FftGeom<M1, M2>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
+#if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
+#else
+    const double* TW = tab;
+#endif
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
     };
+#if FOTO_FFT_TW_LDS
     for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
+#endif
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double is0 = 1.0 / PB[2 * (M + 1)], is = 1.0 / PB[2 * (M + 1) + 1];
     // Z_k from X_k, X_{N-k}, X_{M-k}, X_{M+k}, read straight from global (L2-resident lines;
     // no LDS image of X, so Z is written once and nothing is held in registers across a barrier)
-    for (int idx = tid; idx < LPB * M; idx += 256) {
+    using RP = FftRounds<LPB * M>;
+    double xk[RP::R], xnk[RP::R], xmk[RP::R], xpk[RP::R];   // X_k, X_{N-k}, X_{M-k}, X_{N-M+k}
+#pragma unroll
+    for (int j0 = 0; j0 < RP::R; ++j0) {   // all rounds' loads first
+        const int idx = tid + 256 * j0;
+        int l, k;
+        if (CONTIG) { l = idx / M; k = idx - l * M; }
+        else { k = idx / LPB; l = idx - k * LPB; }
+        xk[j0] = xnk[j0] = xmk[j0] = xpk[j0] = 0.0;
+        if (RP::ok(idx) && l < f.nl) {
+            const double* X = in + base(l);
+            xk[j0] = X[k * st];
+            if (k != 0) xnk[j0] = X[(N - k) * st];
+            xmk[j0] = X[(M - k) * st];
+            if (M - k != 0) xpk[j0] = X[(N - (M - k)) * st];
+        }
+    }
+#pragma unroll
+    for (int j0 = 0; j0 < RP::R; ++j0) {
+        const int idx = tid + 256 * j0;
+        if (!RP::ok(idx)) continue;
         int l, k;
         if (CONTIG) { l = idx / M; k = idx - l * M; }
         else { k = idx / LPB; l = idx - k * LPB; }
         double zr = 0.0, zi = 0.0;
         if (l < f.nl) {
-            const double* X = in + base(l);
             // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
-            auto V = [&](int j, double& vr, double& vi) {
-                const double yr = X[j * st] * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -X[(N - j) * st] * is;
+            auto V = [&](int j, double xj, double xnj, double& vr, double& vi) {
+                const double yr = xj * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -xnj * is;
                 const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
                 vr = fma(wbr, yr, -wbi * yi);
                 vi = fma(wbr, yi, wbi * yr);
             };
             double ar, ai, br, bi;
-            V(k, ar, ai);
-            V(M - k, br, bi);
+            V(k, xk[j0], xnk[j0], ar, ai);
+            V(M - k, xmk[j0], xpk[j0], br, bi);
             bi = -bi;                                                  // conj V_{M-k} = V_{k+M}
             const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_k
             const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
@@ -854,7 +923,11 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     fft_stage2<M1, M2, true, LPB>(L);
     __syncthreads();
     constexpr double iM = 1.0 / M;
-    for (int idx = tid; idx < LPB * N; idx += 256) {   // x_i = v_p, p = Makhoul position of i
+    using RS = FftRounds<LPB * N>;
+#pragma unroll
+    for (int j0 = 0; j0 < RS::R; ++j0) {   // x_i = v_p, p = Makhoul position of i
+        const int idx = tid + 256 * j0;
+        if (!RS::ok(idx)) continue;
         int l, i;
         if (CONTIG) { l = idx / N; i = idx - l * N; }
         else { i = idx / LPB; l = idx - i * LPB; }
