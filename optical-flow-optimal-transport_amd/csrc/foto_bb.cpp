@@ -115,7 +115,7 @@ struct foto_bb_ctx {
     double prev_crit = -1;
     foto_bb_stats st{};
     KTimer kt;
-    hipEvent_t ph[2] = {nullptr, nullptr};
+    hipEvent_t ph[4] = {nullptr, nullptr, nullptr, nullptr};   // phase boundaries (rhs | cg | prox)
     ~foto_bb_ctx() {
         sh.clear();
         if (nc) (void)ncclCommDestroy(nc);
@@ -435,22 +435,13 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
         c->kt.stop(e, c->s, FOTO_K_RHS, 56.0 * nv);
     }
     FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    // phase boundaries are recorded, not waited on: the one host wait per outer iteration
+    // is the crit readback below (a wait here idled the GPU for the host's wake-up)
     FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
-    float t_rhs = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->ph[0], c->ph[1]));
-    c->st.ms_rhs += t_rhs;
-
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
     FOTO_TRY(cg_solve(c, cg_iters, cg_info));
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
-    float t_cg = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[0], c->ph[1]));
-    c->st.ms_cg += t_cg;
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[2], c->s));
     c->have_phi = 1;
 
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
     FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
     for (auto& sp : c->sh) {
         Shard& s = *sp;
@@ -462,10 +453,14 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
     }
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
     FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
-    float t_prox = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, c->ph[0], c->ph[1]));
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
+    float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->ph[0], c->ph[1]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[1], c->ph[2]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, c->ph[2], c->ph[3]));
+    c->st.ms_rhs += t_rhs;
+    c->st.ms_cg += t_cg;
     c->st.ms_prox += t_prox;
     c->kt.resolve();
 

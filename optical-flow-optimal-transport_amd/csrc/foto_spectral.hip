@@ -1259,6 +1259,70 @@ __device__ __forceinline__ double plan_mul_lam(double U, double c0, double c1, d
     return (lane < NG) ? c0 * U + c1 * X : 0.0;
 }
 
+// Register-only variants (FOTO_PLAN_DPP): V broadcast by v_readlane into SGPRs, the |terms|
+// sums by FMA with |.| operand modifiers, lane sums by a DPP row_shr tree (lanes 15 and 31
+// hold the row totals), neighbours for lam U by DPP wave shifts -- no LDS round trip.
+#ifndef FOTO_PLAN_DPP
+#define FOTO_PLAN_DPP 1
+#endif
+
+__device__ __forceinline__ double dbl_readlane(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dbl_dpp(double v) {   // lanes without a source read 0
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// sum over lanes 0 .. 31 (lanes >= NG hold 0), uniform result: row_shr 1, 2, 4, 8 tree
+__device__ __forceinline__ double dpp_sum32(double v) {
+    v += dbl_dpp<0x111>(v);
+    v += dbl_dpp<0x112>(v);
+    v += dbl_dpp<0x114>(v);
+    v += dbl_dpp<0x118>(v);
+    return dbl_readlane(v, 15) + dbl_readlane(v, 31);
+}
+
+__device__ __forceinline__ double plan_ip_dpp(double U, double V, const double (&hrow)[NG], double* cratio) {
+    double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < NG; c += 2) {
+        const double v0 = dbl_readlane(V, c);
+        w0 = fma(hrow[c], v0, w0);
+        a0 = fma(fabs(hrow[c]), fabs(v0), a0);
+        if (c + 1 < NG) {
+            const double v1 = dbl_readlane(V, c + 1);
+            w1 = fma(hrow[c + 1], v1, w1);
+            a1 = fma(fabs(hrow[c + 1]), fabs(v1), a1);
+        }
+    }
+    const double s = dpp_sum32(U * (w0 + w1));
+    const double sa = dpp_sum32(fabs(U) * (a0 + a1));
+    *cratio = (s != 0.0) ? sa / fabs(s) : INFINITY;
+    return s;
+}
+
+__device__ __forceinline__ double plan_mul_lam_dpp(double U, double c0, double c1) {
+    const int lane = threadIdx.x & 63;
+    const double um = dbl_dpp<0x138>(U);   // wave_shr:1 -> U[lane - 1]
+    const double up = dbl_dpp<0x130>(U);   // wave_shl:1 -> U[lane + 1]
+    const int pb = (lane < NCO) ? 0 : NCO, m = lane - pb;
+    double X = 0.0;
+    if (lane < NG) {
+        if (m == 1) X += um;
+        if (m >= 2) X += 0.5 * um;
+        if (m <= NCO - 3) X += 0.5 * up;
+    }
+    return (lane < NG) ? c0 * U + c1 * X : 0.0;
+}
+
 // Finish the pass's bookkeeping and plan the next pass (scipy's loop: top-of-iteration test
 // ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p).  Called by all 64
 // lanes of one wave with the same S (state at the start of the pass) and the summed
@@ -1303,15 +1367,24 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         double rho, cr = 0.0;
         if (i == 0) rho = tot[0];
         else {
+#if FOTO_PLAN_DPP
+            rho = plan_ip_dpp(R, R, hrow, &cr);
+#else
             rho = plan_ip(R, R, hrow, xb, &cr);
+#endif
             if (!(cr <= S_CLIM)) break;   // badly conditioned (or NaN): leave it to the next pass
         }
         if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
         const bool first = (S.k + i == 0);
         const double beta = first ? 0.0 : rho / rho_prev;
         const double Pn = first ? R : beta * P + R;
+#if FOTO_PLAN_DPP
+        const double Q = plan_mul_lam_dpp(Pn, S.c0, S.c1);
+        const double den = plan_ip_dpp(Pn, Q, hrow, &cr);
+#else
         const double Q = plan_mul_lam(Pn, S.c0, S.c1, xb);
         const double den = plan_ip(Pn, Q, hrow, xb, &cr);
+#endif
         if (i > 0 && !(cr <= S_CLIM)) break;
         const double alpha = rho / den;
         R = R - alpha * Q;
@@ -1711,6 +1784,8 @@ static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, s
     }
 }
 
+static int reset_s2(SpecImpl* P, hipStream_t s);
+
 int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, int sstep, hipStream_t s) {
     if (sstep != 1 && sstep != 2) {
         set_error("spectral CG: s-step must be 1 or 2");
@@ -1831,7 +1906,7 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
     FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS2, sizeof(SStep)));
-    (void)s;
+    FOTO_TRY(reset_s2(P, s));   // c0, c1 for the fused INIT (solve_tcol)
     return 0;
 }
 
@@ -1911,7 +1986,6 @@ static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* i
                     hipStream_t s, bool init_done = false) {
     const double N = P->nbox();
     if (!init_done) {
-        FOTO_TRY(reset_s2(P, s));
         hipEvent_t e = kt ? kt->start(s) : nullptr;
         FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, nullptr, s));
         if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * N);
@@ -1976,7 +2050,8 @@ static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxite
                       int* info, KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
-    FOTO_TRY(reset_s2(P, s));
+    // no reset_s2 here (a host wait per solve): the INIT plan rewrites every field but the
+    // constant c0, c1, which init() set
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
     FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, b, s));
@@ -2065,7 +2140,6 @@ int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
 
 int SpectralPlan::cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
-    FOTO_TRY(reset_s2(P, s));
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, P->gath, s));
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * P->nbox());
