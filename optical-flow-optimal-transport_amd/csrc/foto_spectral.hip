@@ -1191,8 +1191,20 @@ struct SStep {
     double a[SMAX], b[SMAX];
     double rho_prev;   // rho_{k-1}
     double atol;
-    double c0, c1;
+    double c0, c1;     // Chebyshev interval of the next pass's moments: lam in [c0 - c1, c0 + c1]
+    double gc0, gc1;   // the whole spectrum's interval (fixed; every solve's INIT moments use it)
 };
+
+// Interval adaptation: the Chebyshev-Krylov basis is well conditioned when [c0 - c1, c0 + c1]
+// spans where the residual measure sum r^2 delta(lam) has its weight.  Early in a solve that
+// weight sits at low frequencies and the full-spectrum basis is nearly degenerate (passes of
+// 1-2 steps); so the plan sets the next pass's interval to [lmin, min(lmax, mean + S_KAPPA sd)]
+// of the measure of the state it just received (from M_0..M_2 of the rr family).  Elements
+// above the interval get |x| > 1 (large T_m); the cancellation rule keeps every planned step
+// accurate regardless.  Measured (numpy restatement, tests/test_sstep_plan.py): at the bench
+// grid 24 -> 22 passes on the first outer iteration, 33 -> 28 at 160x120x32; no change in
+// CG counts or iterates.
+constexpr double S_KAPPA = 2.0;
 
 // Plan helpers.  Coefficient vectors are distributed one entry per lane: lane j < NG holds
 // index j of (r part | q part), lanes >= NG hold 0; lane j also holds row j of the Gram
@@ -1331,6 +1343,8 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
                                 double rtol, int maxiter) {
     const int lane = threadIdx.x & 63;
     if (init) {
+        S.c0 = S.gc0;   // the INIT moments were taken over the whole spectrum
+        S.c1 = S.gc1;
         S.k = 0;
         S.rho_prev = 0.0;
         S.atol = fmax(0.0, rtol * sqrt(tot[0]));   // scipy: max(atol, rtol * ||b||)
@@ -1406,9 +1420,23 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         S.iters = conv ? S.k + n : maxiter;
         if (n == 0) S.done = conv ? 1 : 2;   // nothing left to apply
     }
+    // next pass's interval, from the measure of the state these moments describe
+    double nc0 = S.c0, nc1 = S.c1;
+    if (tot[0] > 0.0) {
+        const double ex = tot[1] / tot[0], ex2 = 0.5 * (tot[2] + tot[0]) / tot[0];
+        const double mean = S.c0 + S.c1 * ex, sd = S.c1 * sqrt(fmax(ex2 - ex * ex, 0.0));
+        const double lmin = S.gc0 - S.gc1, lmax = S.gc0 + S.gc1;
+        double hi = fmin(lmax, mean + S_KAPPA * sd);
+        hi = fmax(hi, lmin + 1e-3 * (lmax - lmin));
+        if (hi == hi) {   // not NaN
+            nc0 = 0.5 * (hi + lmin);
+            nc1 = 0.5 * (hi - lmin);
+        }
+    }
     if (lane == 0) {   // scalars only: a[], b[] were stored above
         Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
         Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
+        Sg->c0 = nc0; Sg->c1 = nc1;
     }
 }
 
@@ -1459,7 +1487,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
     const SStep S0 = *Sg;             // uniform: scalar loads
     if (!INIT && (S0.done || S0.nsteps == 0)) return;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
-    const double c0 = S0.c0, ic1 = 1.0 / S0.c1;
+    const double c0 = INIT ? S0.gc0 : S0.c0, ic1 = 1.0 / (INIT ? S0.gc1 : S0.c1);
     const bool loadq = !INIT && k > 0;
     // r_0 = b^: the INIT pass (or the fused t-axis kernel, which writes no r^) leaves it in b^
     const double* src = (INIT || k == 0) ? bh : rh;
@@ -1544,6 +1572,203 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
     sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
 }
 
+// ---------------------------------------------------------------------------- ring-fed pass
+// The same pass with r, q streamed through a per-wave LDS ring by LDS-DMA
+// (global_load_lds_dwordx4): each wave walks its own sequence of 128-column row segments
+// ("wave tiles") and keeps D of them in flight, so a CU holds up to 16 x (D - 1) x 2 KiB of
+// loads in flight without spending VGPRs on them (the register-fed pass, 121 VGPRs for the
+// 48 moment accumulators, holds one tile per wave: ~32 KiB per CU, too little to cover the
+// HBM latency under load -- it streamed at ~4.3 TB/s).  Counting: VMEM operations complete
+// in issue order on gfx950 (stores included), so before reading tile j the wave waits until
+// at most K operations are outstanding, K = those issued after tile j's loads.  The ring is
+// read with inline-asm ds_read (invisible to hipcc's waitcnt pass, which would otherwise wait
+// for the newest DMA), and the loop has no other vector-memory loads: the mu tables are
+// staged in LDS before the pipeline starts (an ordinary load would complete behind every
+// DMA in flight).  Per element the arithmetic is the register-fed pass's, in the same order:
+// r, q are bit-identical; only the moment summation order differs (element-to-thread map).
+#ifndef FOTO_RING_D
+#define FOTO_RING_D 4
+#endif
+constexpr int RING_NW = S2_NTH / 64;    // waves per block
+constexpr int RING_SLOT = 256;          // doubles per ring slot: r (128) then q (128)
+constexpr int RING_TAB = 2304;          // mu_x, mu_t, mu_y (own rows) staged in LDS (doubles)
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ unsigned lds_u32(const void* p) { return (unsigned)(uintptr_t)(const lds_void_t*)p; }
+
+__device__ __forceinline__ dbl2 lds_ld128(unsigned a) {   // caller waits lgkmcnt
+    dbl2 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ double lds_ld64(unsigned a) {
+    double v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+// wait until at most k vector-memory operations are outstanding (k wave-uniform; clamped)
+__device__ __forceinline__ void vm_wait(int k) {
+    switch (k) {
+#define FOTO_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        FOTO_VMW(1) FOTO_VMW(2) FOTO_VMW(3) FOTO_VMW(4) FOTO_VMW(5) FOTO_VMW(6) FOTO_VMW(7) FOTO_VMW(8)
+        FOTO_VMW(9) FOTO_VMW(10) FOTO_VMW(11) FOTO_VMW(12) FOTO_VMW(13) FOTO_VMW(14) FOTO_VMW(15)
+#undef FOTO_VMW
+        default:
+            if (k > 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+// Usable for a shard when Nx is even (16-B lanes) and the tables fit.
+static inline bool ring_ok(const SpecTab& T) {
+    return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB;
+}
+
+template <int D, bool INIT, bool FUSE>
+__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_spec_s2r(
+        SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
+        RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
+    __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
+    const SStep S0 = *Sg;
+    if (!INIT && (S0.done || S0.nsteps == 0)) return;
+    const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
+    const double c0 = INIT ? S0.gc0 : S0.c0, ic1 = 1.0 / (INIT ? S0.gc1 : S0.c1);
+    const bool loadq = !INIT && k > 0;
+    const double* src = (INIT || k == 0) ? bh : rh;
+    // tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl)
+    double* tab = ring + RING_NW * D * RING_SLOT;
+    for (int i = threadIdx.x; i < T.Nx + T.Nt + T.nyl; i += S2_NTH)
+        tab[i] = (i < T.Nx) ? T.mx[i] : (i < T.Nx + T.Nt) ? T.mt[i - T.Nx] : T.my[T.y0 + i - T.Nx - T.Nt];
+    __syncthreads();
+    const unsigned tab_a = lds_u32(tab);
+
+    double acc[NACC];
+#pragma unroll
+    for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
+    auto moments = [&](double lam, double r, double q) {
+        const double x = (lam - c0) * ic1, x2 = x + x;
+        const double rr = r * r, rq = r * q, qq = q * q;
+        acc[0] += rr;
+        acc[NMOM] += rq;
+        acc[2 * NMOM] += qq;
+        acc[1] = fma(x, rr, acc[1]);
+        acc[NMOM + 1] = fma(x, rq, acc[NMOM + 1]);
+        acc[2 * NMOM + 1] = fma(x, qq, acc[2 * NMOM + 1]);
+        double tm2 = 1.0, tm1 = x;
+#pragma unroll
+        for (int m = 2; m < NMOM; ++m) {
+            const double t = fma(x2, tm1, -tm2);
+            acc[m] = fma(t, rr, acc[m]);
+            acc[NMOM + m] = fma(t, rq, acc[NMOM + m]);
+            acc[2 * NMOM + m] = fma(t, qq, acc[2 * NMOM + m]);
+            tm2 = tm1;
+            tm1 = t;
+        }
+    };
+
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int rows = T.Nt * T.nyl, ntx = (T.Nx + 127) / 128;
+    const int nwt = rows * ntx;
+    const int gw = blockIdx.x * RING_NW + w, W = gridDim.x * RING_NW;
+    const int nj = gw < nwt ? (nwt - 1 - gw) / W + 1 : 0;
+    double* wring = ring + w * D * RING_SLOT;
+    const int g = loadq ? 2 : 1;             // DMA instructions per tile
+    constexpr int NS = INIT ? 1 : 2;         // store instructions per tile
+    auto tile_of = [&](int j, int& row, int& cx) {
+        const int u = gw + j * W;
+        row = u / ntx;
+        cx = u - row * ntx;
+    };
+    auto issue = [&](int j) {
+        int row, cx;
+        tile_of(j, row, cx);
+        int kx = cx * 128 + 2 * lane;
+        if (kx >= T.Nx) kx = cx * 128;   // idle lanes fetch a valid address; never read
+        const int64_t i = (int64_t)row * T.Nx + kx;
+        double* slot = wring + (j % D) * RING_SLOT;
+        __builtin_amdgcn_global_load_lds((const void*)(src + i), (lds_void_t*)slot, 16, 0, 0);
+        if (loadq) __builtin_amdgcn_global_load_lds((const void*)(ph + i), (lds_void_t*)(slot + 128), 16, 0, 0);
+    };
+    for (int j = 0; j < D - 1 && j < nj; ++j) issue(j);
+    for (int j = 0; j < nj; ++j) {
+        if (j + D - 1 < nj) issue(j + D - 1);
+        const int nG = min(j + D - 1, nj - 1) - j, nS = min(j, D - 1);
+        vm_wait(g * nG + NS * nS);
+        int row, cx;
+        tile_of(j, row, cx);
+        const int kx = cx * 128 + 2 * lane;
+        const unsigned sa = lds_u32(wring + (j % D) * RING_SLOT) + 16 * lane;
+        dbl2 rv = lds_ld128(sa);
+        dbl2 qv = loadq ? lds_ld128(sa + 1024) : dbl2{0.0, 0.0};
+        const int kt = row / T.nyl, ky = row - kt * T.nyl;
+        double mtv = lds_ld64(tab_a + 8 * (T.Nx + kt));
+        double myv = lds_ld64(tab_a + 8 * (T.Nx + T.Nt + ky));
+        const bool ok = kx < T.Nx;
+        dbl2 mxv = lds_ld128(tab_a + 8 * (ok ? kx : 0));
+        // the wait names every asm-loaded register, so no use is scheduled above it
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rv), "+v"(qv), "+v"(mtv), "+v"(myv), "+v"(mxv) :: "memory");
+        const double rowmu = mtv + myv;
+        const double l0 = T.reps + T.r * (rowmu + mxv[0]);
+        const double l1 = T.reps + T.r * (rowmu + mxv[1]);
+        double r0 = rv[0], r1 = rv[1], q0 = qv[0], q1 = qv[1];
+        const int64_t i = (int64_t)row * T.Nx + kx;
+        if (INIT) {
+            if (ok) *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
+        } else {
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+                if (s >= ns) break;
+                const double a = S0.a[s], b = S0.b[s];
+                const double p0 = (k + s == 0) ? r0 : fma(b, q0, r0);
+                const double p1 = (k + s == 0) ? r1 : fma(b, q1, r1);
+                r0 = fma(-a, l0 * p0, r0);
+                r1 = fma(-a, l1 * p1, r1);
+                q0 = p0;
+                q1 = p1;
+            }
+            if (ok) {
+                *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
+                *reinterpret_cast<dbl2*>(ph + i) = dbl2{q0, q1};
+            }
+        }
+        if (ok) {
+#if defined(FOTO_RING_ABLATE)   // timing studies only (tools/pass_lab.hip): no moments
+            acc[0] += r0 * q0 + r1 * q1 + l0 * l1;
+#else
+            moments(l0, r0, q0);
+            moments(l1, r1, q1);
+#endif
+        }
+    }
+    __shared__ double tot[NACC];
+    if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
+    if (!FUSE) {
+        for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
+        return;
+    }
+    if (threadIdx.x >= 64) return;
+    __shared__ double xb[3 * NG + 2];
+    sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
+}
+
+// host launcher (D = 0: FOTO_RING_D)
+static hipError_t launch_s2_ring(const SpecTab& T, double* rh, double* ph, const double* bh, SStep* Sg, RedBuf rb,
+                                 double rtol, int maxiter, double* gath, int rank, bool init, bool fuse, int D,
+                                 int nb = 256, hipStream_t s = 0) {
+    if (D == 0) D = FOTO_RING_D;
+#define FOTO_RL(DD, I, F) k_spec_s2r<DD, I, F><<<nb, S2_NTH, 0, s>>>(T, rh, ph, bh, Sg, rb, rtol, maxiter, gath, rank)
+#define FOTO_RL_D(DD)                                                    \
+    if (D == DD) {                                                       \
+        if (init) { if (fuse) FOTO_RL(DD, true, true); else FOTO_RL(DD, true, false); } \
+        else { if (fuse) FOTO_RL(DD, false, true); else FOTO_RL(DD, false, false); }    \
+    }
+    FOTO_RL_D(2) else FOTO_RL_D(3) else FOTO_RL_D(4) else return hipErrorInvalidValue;
+#undef FOTO_RL_D
+#undef FOTO_RL
+    return hipGetLastError();
+}
+
 // Multi-shard planning step (one wave): moments summed over ranks in rank order.
 __global__ __launch_bounds__(64) void k_spec_s2_plan(SStep* Sg, const double* __restrict__ gath, int world, int init,
                                                      double rtol, int maxiter) {
@@ -1589,7 +1814,7 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
     const int64_t ncols = (int64_t)T.nyl * T.Nx;
     const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
     const SStep S0 = *Sg;
-    const double c0 = S0.c0, ic1 = 1.0 / S0.c1;
+    const double c0 = S0.gc0, ic1 = 1.0 / S0.gc1;   // INIT: the whole spectrum
     double acc[NMOM];
 #pragma unroll
     for (int m = 0; m < NMOM; ++m) acc[m] = 0.0;
@@ -1736,6 +1961,8 @@ struct SpecImpl {
     SStep* S2 = nullptr;
     SStep* hS2 = nullptr;
     int nblocks2 = 0;
+    bool ring = false;   // s-step passes by the LDS-ring kernel
+    int nb_ring = 0;
     double* Cth = nullptr;        // t-axis DCT-II even | odd halves (column kernels)
     bool tcol = false;            // single shard, s-step, Nt in FOTO_TCOL_SIZES
     int tcol_nb = 0;              // column kernels' blocks
@@ -1876,6 +2103,12 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         const char* e = getenv("FOTO_S2_BLOCKS");   // tuning knob for A/B runs
         const int want = e ? std::max(1, atoi(e)) : std::max(1, per_cu) * cus;
         P->nblocks2 = std::min(ntiles2, want);
+        // ring-fed pass (k_spec_s2r): one 1024-thread block per CU (its LDS ring), at most one
+        // block per 16 wave tiles; FOTO_RING=0 selects the register-fed pass (A/B runs)
+        const char* er = getenv("FOTO_RING");
+        P->ring = ring_ok(P->tab()) && !(er && atoi(er) == 0);
+        const int nwt = ((g.Nx + 127) / 128) * rows;
+        P->nb_ring = std::max(1, std::min({P->nblocks2, cus, (nwt + RING_NW - 1) / RING_NW}));
     }
     {
         const char* e = getenv("FOTO_TCOL");   // 0: t axis by dct_pass + separate INIT / xhat passes (A/B runs)
@@ -1954,6 +2187,13 @@ static hipError_t launch_s2(SpecImpl* P, bool init, double rtol, int maxiter, do
     // gath == nullptr: single shard, fused plan (or the separate plan kernel, FOTO_S2_SPLIT=1)
     const bool fuse = (gath == nullptr) && !P->split_plan;
     double* gw = gath ? gath : P->gath;
+    if (P->ring) {
+        const hipError_t e = launch_s2_ring(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gw, P->rank, init, fuse,
+                                            FOTO_RING_D, P->nb_ring, s);
+        if (e != hipSuccess || gath != nullptr || fuse) return e;
+        k_spec_s2_plan<<<1, 64, 0, s>>>(P->S2, P->gath, 1, init ? 1 : 0, rtol, maxiter);
+        return hipGetLastError();
+    }
 #define FOTO_S2_LAUNCH(V, I, F) \
     k_spec_s2<V, I, F><<<nb, S2_NTH, 0, s>>>(T, P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, gw, P->rank)
     if (P->vec()) {
@@ -1975,6 +2215,8 @@ static int reset_s2(SpecImpl* P, hipStream_t s) {
     SStep h{};
     h.c0 = P->c0;
     h.c1 = P->c1;
+    h.gc0 = P->c0;
+    h.gc1 = P->c1;
     *P->hS2 = h;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->S2, P->hS2, sizeof(SStep), hipMemcpyHostToDevice, s));
     FOTO_HIP_CHECK(hipStreamSynchronize(s));   // hS2 is reused by polling

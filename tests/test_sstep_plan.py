@@ -3,7 +3,9 @@
 csrc/foto_spectral.hip runs scipy's CG recurrence (benamou_brenier.py:85 ->
 scipy.sparse.linalg.cg) in the DCT eigenbasis, where A = C^T diag(lam) C and every CG
 update is pointwise.  One pass applies up to SMAX = 8 iterations whose scalars were planned
-from Chebyshev moments of the pass-start state (r_k, p_{k-1}); step i > 0 is taken only
+from Chebyshev moments of the pass-start state (r_k, p_{k-1}) over an interval adapted to
+the residual measure (whole spectrum at INIT, then [lmin, mean + 2 sd] of the previous
+pass's measure); step i > 0 is taken only
 while its two Gram-form inner products have cancellation ratio sum|terms| / |value| <=
 S_CLIM = 1e4, and the moments are summed with compensated block reductions (correctly
 rounded to ~1 ulp).  This module restates that rule on the CPU (test infrastructure: the
@@ -26,6 +28,7 @@ SMAX = 8
 NMOM = 2 * SMAX
 NCO = SMAX + 1
 S_CLIM = 1e4
+S_KAPPA = 2.0
 
 
 def _lam(Nt, Ny, Nx, r, eps):
@@ -95,25 +98,37 @@ def _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter):
     return al, be, False, rho_prev
 
 
+def _next_interval(Mrr, c0, c1, lmin, lmax):
+    """Next pass's Chebyshev interval [lmin, min(lmax, mean + S_KAPPA sd)] of the residual
+    measure the moments describe (csrc/foto_spectral.hip sstep_plan_wave)."""
+    if not Mrr[0] > 0:
+        return c0, c1
+    ex, ex2 = Mrr[1] / Mrr[0], 0.5 * (Mrr[2] + Mrr[0]) / Mrr[0]
+    mean, sd = c0 + c1 * ex, c1 * math.sqrt(max(ex2 - ex * ex, 0.0))
+    hi = max(min(lmax, mean + S_KAPPA * sd), lmin + 1e-3 * (lmax - lmin))
+    return 0.5 * (hi + lmin), 0.5 * (hi - lmin)
+
+
 def sstep_cg(b, Nt, Ny, Nx, r, eps, rtol=1e-6, maxiter=1000, stats=None):
     """x, info, iterations -- scipy's contract (x0 = 0, M = I)."""
     lam = _lam(Nt, Ny, Nx, r, eps)
     lmin, lmax = lam.min(), lam.max()   # r eps, r eps + r (mu_t + mu_y + mu_x)_max
-    c0, c1 = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
-    x = (lam - c0) / c1
-    T = np.empty((NMOM, lam.size))
-    T[0] = 1.0
-    T[1] = x
-    for m in range(2, NMOM):
-        T[m] = 2 * x * T[m - 1] - T[m - 2]
+    c0, c1 = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)   # INIT: the whole spectrum
     bh = sfft.dctn(b.reshape(Nt, Ny, Nx), norm="ortho").ravel()
     rr, q = bh.copy(), np.zeros_like(bh)
     atol = max(0.0, rtol * math.sqrt(math.fsum(bh * bh)))
     k, rho_prev, passes, conv = 0, 0.0, 0, False
     while k < maxiter:
+        x = (lam - c0) / c1
+        T = np.empty((NMOM, lam.size))
+        T[0] = 1.0
+        T[1] = x
+        for m in range(2, NMOM):
+            T[m] = 2 * x * T[m - 1] - T[m - 2]
         Mrr, Mrq, Mqq = _moments(T, rr * rr), _moments(T, rr * q), _moments(T, q * q)
         al, be, conv, rho_prev = _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter)
         passes += 1
+        c0, c1 = _next_interval(Mrr, c0, c1, lmin, lmax)
         for a, bt in zip(al, be):
             p = rr.copy() if k == 0 else bt * q + rr
             rr = rr - a * (lam * p)

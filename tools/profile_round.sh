@@ -10,10 +10,10 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out
 rm -rf $O/prof_kt $O/prof_fetch $O/prof_write $O/cal_fetch $O/cal_write
 timeout -k 10 240 python3 bench.py $args > $O/bench_full.log 2>&1 || exit $?
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_kt -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_kt.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_fetch.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_write.log 2>&1 || exit $?
-timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d $O/cal_fetch -o run -- tools/calib_fetch > $O/cal_fetch.log 2>&1 || exit $?
-timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d $O/cal_write -o run -- tools/calib_fetch > $O/cal_write.log 2>&1 || exit $?
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_kt -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_kt.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/prof_fetch -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_fetch.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/prof_write -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_write.log 2>&1 || exit $?
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/cal_fetch -o run -- tools/calib_fetch > $O/cal_fetch.log 2>&1 || exit $?
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/cal_write -o run -- tools/calib_fetch > $O/cal_write.log 2>&1 || exit $?
 python3 tools/summarize_profile.py --tag "$tag" --kt $O/prof_kt --fetch $O/prof_fetch --write $O/prof_write \
     --calib-fetch $O/cal_fetch --calib-write $O/cal_write --bench $O/bench_full.log --out $O/profiles_new

@@ -25,14 +25,15 @@ SHORT = {
     # first match wins: the specific names before their prefixes
     "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox": "prox", "k_rhs": "rhs",
     "k_spec_s2_plan": "spec_plan", "k_spec_s2": "spec_cg", "k_spec_init": "spec_init", "k_spec_xhat": "spec_xhat",
-    "k_spec_cg": "spec_cg1", "k_dct_fft": "dct_fft", "k_dct": "dct_gemm", "k_traj": "flow",
+    "k_spec_cg": "spec_cg1", "k_dct_fft_fwd": "dct_fft_fwd", "k_dct_fft_inv": "dct_fft_inv",
+    "k_dct_t_fwd_init": "dct_t_init", "k_dct_t_inv_xhat": "dct_t_xhat", "k_dct": "dct_gemm", "k_traj": "flow",
     "k_gn_pcg_dir": "gn_dir", "k_gn_pcg_upd": "gn_upd",
 }
 
 
 # bytes per lane of each hot kernel's streaming loads (csrc/*.hip)
 LOAD_WIDTH = {"spec_cg": 16, "spec_cg1": 16, "spec_init": 16, "spec_xhat": 16, "cg_upd": 8, "cg_dir": 8, "prox": 8,
-              "rhs": 8, "dct_fft": 8, "dct_gemm": 8, "flow": 8,
+              "rhs": 8, "dct_fft_fwd": 8, "dct_fft_inv": 8, "dct_t_init": 8, "dct_t_xhat": 8, "dct_gemm": 8, "flow": 8,
               "gn_dir": 8, "gn_upd": 8}
 CALIB_BYTES = {"rd8": 2 << 30, "rd16": 2 << 30, "wr8": 1 << 30, "wr16": 1 << 30}
 
@@ -52,11 +53,19 @@ def short(name):
 
 
 def pmc(dirname, counter):
+    """Mean counter value per launch of each kernel.  Launches below 1 % of that kernel's
+    median are no-ops (s-step passes launched past the end of a solve exit at once) and are
+    left out, so the figure describes a working launch."""
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(find_csv(dirname, "counter_collection.csv"))):
         if r["Counter_Name"] == counter:
             agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+    out, cnt = {}, {}
+    for k, v in agg.items():
+        med = sorted(v)[len(v) // 2]
+        w = [x for x in v if x >= 0.01 * med] or v
+        out[k], cnt[k] = sum(w) / len(w), len(w)
+    return out, cnt
 
 
 def main():
