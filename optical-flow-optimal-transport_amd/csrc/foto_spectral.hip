@@ -1213,7 +1213,8 @@ constexpr double S_KAPPA = 2.0;
 // write-completion wait.
 #define FOTO_LDS_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-// <U, V> = sum_j U_j (H V)_j and its cancellation ratio sum |terms| / |<U, V>|; lanes 0 and
+// <U, V> = sum_j U_j (H V)_j and whether its cancellation ratio sum |terms| / |<U, V>| is
+// within S_CLIM (*cratio = 1, else infinity; tested as sum|terms| <= S_CLIM |<U, V>|); lanes 0 and
 // 1 sum the NG lane values (value, |terms|) in lane order, every lane reads the result.
 __device__ __forceinline__ double plan_ip(double U, double V, const double (&hrow)[NG], double* xb, double* cratio) {
     const int lane = threadIdx.x & 63;
@@ -1249,7 +1250,7 @@ __device__ __forceinline__ double plan_ip(double U, double V, const double (&hro
     FOTO_LDS_WAIT();
     const double s = xb[3 * NG], sa = xb[3 * NG + 1];
     FOTO_LDS_WAIT();
-    *cratio = (s != 0.0) ? sa / fabs(s) : INFINITY;
+    *cratio = (s != 0.0 && sa <= S_CLIM * fabs(s)) ? 1.0 : INFINITY;   // (no division)
     return s;
 }
 
@@ -1302,24 +1303,52 @@ __device__ __forceinline__ double dpp_sum32(double v) {
     return dbl_readlane(v, 15) + dbl_readlane(v, 31);
 }
 
-__device__ __forceinline__ double plan_ip_dpp(double U, double V, const double (&hrow)[NG], double* cratio) {
+// nc: V's coefficients of degree >= nc are zero in both parts (step i of a plan: R has degree
+// i, lam Pn degree i + 1); with the step loop unrolled nc is a constant and the zero columns
+// cost nothing (about half the broadcasts and FMAs of a plan).
+__device__ __forceinline__ double plan_ip_dpp(double U, double V, const double (&hrow)[NG], double* cratio,
+                                              int nc = NCO) {
     double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+    int j = 0;
 #pragma unroll
-    for (int c = 0; c < NG; c += 2) {
-        const double v0 = dbl_readlane(V, c);
-        w0 = fma(hrow[c], v0, w0);
-        a0 = fma(fabs(hrow[c]), fabs(v0), a0);
-        if (c + 1 < NG) {
-            const double v1 = dbl_readlane(V, c + 1);
-            w1 = fma(hrow[c + 1], v1, w1);
-            a1 = fma(fabs(hrow[c + 1]), fabs(v1), a1);
+    for (int c = 0; c < NG; ++c) {
+        if (c % NCO >= nc) continue;
+        const double v = dbl_readlane(V, c);
+        if (j++ % 2 == 0) {
+            w0 = fma(hrow[c], v, w0);
+            a0 = fma(fabs(hrow[c]), fabs(v), a0);
+        } else {
+            w1 = fma(hrow[c], v, w1);
+            a1 = fma(fabs(hrow[c]), fabs(v), a1);
         }
     }
     const double s = dpp_sum32(U * (w0 + w1));
     const double sa = dpp_sum32(fabs(U) * (a0 + a1));
-    *cratio = (s != 0.0) ? sa / fabs(s) : INFINITY;
+    *cratio = (s != 0.0 && sa <= S_CLIM * fabs(s)) ? 1.0 : INFINITY;   // (no division)
     return s;
 }
+
+// FOTO_PLAN_DPP == 2: V broadcast through LDS instead (one ds_write, NG/2 broadcast
+// ds_read_b128; the LDS pipe instead of 2 NG v_readlane VALU ops and their hazards).
+__device__ __forceinline__ double plan_ip_lds(double U, double V, const double (&hrow)[NG], double* xb,
+                                              double* cratio) {
+    const int lane = threadIdx.x & 63;
+    if (lane < NG) xb[lane] = V;   // one wave: its LDS operations complete in order
+    double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < NG; c += 2) {
+        const dbl2 v = *reinterpret_cast<const dbl2*>(xb + c);
+        w0 = fma(hrow[c], v[0], w0);
+        a0 = fma(fabs(hrow[c]), fabs(v[0]), a0);
+        w1 = fma(hrow[c + 1], v[1], w1);
+        a1 = fma(fabs(hrow[c + 1]), fabs(v[1]), a1);
+    }
+    const double s = dpp_sum32(U * (w0 + w1));
+    const double sa = dpp_sum32(fabs(U) * (a0 + a1));
+    *cratio = (s != 0.0 && sa <= S_CLIM * fabs(s)) ? 1.0 : INFINITY;   // (no division)
+    return s;
+}
+static_assert(NG % 2 == 0, "pairs of coefficients per broadcast read");
 
 __device__ __forceinline__ double plan_mul_lam_dpp(double U, double c0, double c1) {
     const int lane = threadIdx.x & 63;
@@ -1376,30 +1405,36 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
     double rho_prev = S.rho_prev;
     int n = 0;
     bool conv = false;
+#pragma clang loop unroll(full)
     for (int i = 0; i < SMAX; ++i) {
         if (S.k + i >= maxiter) break;
         double rho, cr = 0.0;
         if (i == 0) rho = tot[0];
         else {
-#if FOTO_PLAN_DPP
-            rho = plan_ip_dpp(R, R, hrow, &cr);
+#if FOTO_PLAN_DPP == 2
+            rho = plan_ip_lds(R, R, hrow, xb, &cr);
+#elif FOTO_PLAN_DPP
+            rho = plan_ip_dpp(R, R, hrow, &cr, i + 1);
 #else
             rho = plan_ip(R, R, hrow, xb, &cr);
 #endif
-            if (!(cr <= S_CLIM)) break;   // badly conditioned (or NaN): leave it to the next pass
+            if (!(cr <= 1.0)) break;   // badly conditioned (or NaN): leave it to the next pass
         }
         if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
         const bool first = (S.k + i == 0);
         const double beta = first ? 0.0 : rho / rho_prev;
         const double Pn = first ? R : beta * P + R;
-#if FOTO_PLAN_DPP
+#if FOTO_PLAN_DPP == 2
         const double Q = plan_mul_lam_dpp(Pn, S.c0, S.c1);
-        const double den = plan_ip_dpp(Pn, Q, hrow, &cr);
+        const double den = plan_ip_lds(Pn, Q, hrow, xb, &cr);
+#elif FOTO_PLAN_DPP
+        const double Q = plan_mul_lam_dpp(Pn, S.c0, S.c1);
+        const double den = plan_ip_dpp(Pn, Q, hrow, &cr, i + 2);
 #else
         const double Q = plan_mul_lam(Pn, S.c0, S.c1, xb);
         const double den = plan_ip(Pn, Q, hrow, xb, &cr);
 #endif
-        if (i > 0 && !(cr <= S_CLIM)) break;
+        if (i > 0 && !(cr <= 1.0)) break;
         const double alpha = rho / den;
         R = R - alpha * Q;
         P = Pn;
@@ -1473,14 +1508,18 @@ __device__ __forceinline__ SpElem spec_elem(const SpecTab& T, int t, int ntx, in
 // 1024 threads: one block per CU at the pass's occupancy (4 waves / SIMD), so the
 // cross-block tail gathers 48 x 256 partials in one round trip (with 256-thread blocks it
 // was 48 x 1024 in six: 14 us of each pass, tools/s2_ablation.hip).
-#ifndef FOTO_S2_NTH
-#define FOTO_S2_NTH 1024
+// Occupancy of the pass kernels follows the accumulator count: 2 SMAX x 3 fp64 moments per
+// thread = 12 SMAX VGPRs (96 at SMAX 8: 4 waves/SIMD in <= 128; 120 at 10: 3 waves in <= 168;
+// 144 at 12: 2 waves), and a block is one CU's worth of waves (one block per CU).
+#ifndef FOTO_S2_WPE
+#define FOTO_S2_WPE (SMAX <= 8 ? 4 : (SMAX <= 10 ? 3 : 2))
 #endif
-constexpr int S2_NTH = FOTO_S2_NTH;   // threads per block of the s-step pass
+constexpr int S2_WPE = FOTO_S2_WPE;                              // waves per SIMD
+constexpr int S2_NTH = 256 * S2_WPE;                            // threads per block of the s-step pass
 
 // 4 waves / SIMD: the streaming body needs the occupancy; the fused plan must fit beside it.
 template <bool VEC, bool INIT, bool FUSE>
-__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
+__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_spec_s2(SpecTab T, double* __restrict__ rh, double* __restrict__ ph,
                                                     const double* __restrict__ bh, SStep* Sg, RedBuf rb,
                                                     double rtol, int maxiter, double* gath, int rank) {
     constexpr int TR = S2_NTH / 64;   // tile = TR rows x 128 columns
@@ -1528,20 +1567,21 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (INIT) {
             st2<VEC>(rh, e.i, e.n2, r0, r1);
         } else {
-#pragma unroll
+#pragma clang loop unroll(full)
             for (int i = 0; i < SMAX; ++i) {
 #if defined(FOTO_S2_ABLATE) && FOTO_S2_ABLATE == 2
-                if (i >= 1) break;
+                if (i >= 1) continue;
 #endif
-                if (i >= ns) break;
-                // iteration k + i: p = beta p + r (p = r at k = 0); r -= alpha (lam p)
-                const double a = S0.a[i], b = S0.b[i];
-                const double p0 = (k + i == 0) ? r0 : fma(b, q0, r0);
-                const double p1 = (k + i == 0) ? r1 : fma(b, q1, r1);
-                r0 = fma(-a, e.l0 * p0, r0);
-                r1 = fma(-a, e.l1 * p1, r1);
-                q0 = p0;
-                q1 = p1;
+                if (i < ns) {   // guard, not break: keeps the loop fully unrolled (S0 out of scratch)
+                    // iteration k + i: p = beta p + r (p = r at k = 0); r -= alpha (lam p)
+                    const double a = S0.a[i], b = S0.b[i];
+                    const double p0 = (k + i == 0) ? r0 : fma(b, q0, r0);
+                    const double p1 = (k + i == 0) ? r1 : fma(b, q1, r1);
+                    r0 = fma(-a, e.l0 * p0, r0);
+                    r1 = fma(-a, e.l1 * p1, r1);
+                    q0 = p0;
+                    q1 = p1;
+                }
             }
             st2<VEC>(rh, e.i, e.n2, r0, r1);
             st2<VEC>(ph, e.i, e.n2, q0, q1);
@@ -1568,7 +1608,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
         return;
     }
     if (threadIdx.x >= 64) return;
-    __shared__ double xb[3 * NG + 2];
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
 }
 
@@ -1586,8 +1626,10 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
 // staged in LDS before the pipeline starts (an ordinary load would complete behind every
 // DMA in flight).  Per element the arithmetic is the register-fed pass's, in the same order:
 // r, q are bit-identical; only the moment summation order differs (element-to-thread map).
+// Ring depth: what the LDS left after the tables (18 KiB) and the reduction scratch allows
+// (16 waves x 4 x 2 KiB at SMAX 8, 12 x 5 at 10, 8 x 8 at 12).
 #ifndef FOTO_RING_D
-#define FOTO_RING_D 4
+#define FOTO_RING_D (S2_WPE == 4 ? 4 : (S2_WPE == 3 ? 5 : 8))
 #endif
 constexpr int RING_NW = S2_NTH / 64;    // waves per block
 constexpr int RING_SLOT = 256;          // doubles per ring slot: r (128) then q (128)
@@ -1613,9 +1655,12 @@ __device__ __forceinline__ void vm_wait(int k) {
 #define FOTO_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
         FOTO_VMW(1) FOTO_VMW(2) FOTO_VMW(3) FOTO_VMW(4) FOTO_VMW(5) FOTO_VMW(6) FOTO_VMW(7) FOTO_VMW(8)
         FOTO_VMW(9) FOTO_VMW(10) FOTO_VMW(11) FOTO_VMW(12) FOTO_VMW(13) FOTO_VMW(14) FOTO_VMW(15)
+        FOTO_VMW(16) FOTO_VMW(17) FOTO_VMW(18) FOTO_VMW(19) FOTO_VMW(20) FOTO_VMW(21) FOTO_VMW(22)
+        FOTO_VMW(23) FOTO_VMW(24) FOTO_VMW(25) FOTO_VMW(26) FOTO_VMW(27) FOTO_VMW(28) FOTO_VMW(29)
+        FOTO_VMW(30) FOTO_VMW(31)
 #undef FOTO_VMW
         default:
-            if (k > 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            if (k > 31) asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
@@ -1625,27 +1670,58 @@ static inline bool ring_ok(const SpecTab& T) {
     return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB;
 }
 
-template <int D, bool INIT, bool FUSE>
-__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_spec_s2r(
-        SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
-        RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
-    __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
-    const SStep S0 = *Sg;
-    if (!INIT && (S0.done || S0.nsteps == 0)) return;
+// Tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl).
+__device__ __forceinline__ void ring_stage_tables(const SpecTab& T, double* tab) {
+    for (int i = threadIdx.x; i < T.Nx + T.Nt + T.nyl; i += S2_NTH)
+        tab[i] = (i < T.Nx) ? T.mx[i] : (i < T.Nx + T.Nt) ? T.mt[i - T.Nx] : T.my[T.y0 + i - T.Nx - T.Nt];
+}
+
+// The wave's tile sequence: u = gw + j W (j < nj), u -> (row, 128-column segment cx).
+struct RingWave {
+    int gw, W, nj, ntx;
+    double* wring;   // this wave's D slots
+};
+
+__device__ __forceinline__ RingWave ring_wave(const SpecTab& T, double* ring, int D) {
+    RingWave w;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int rows = T.Nt * T.nyl;
+    w.ntx = (T.Nx + 127) / 128;
+    const int nwt = rows * w.ntx;
+    w.gw = blockIdx.x * RING_NW + wv;
+    w.W = gridDim.x * RING_NW;
+    w.nj = w.gw < nwt ? (nwt - 1 - w.gw) / w.W + 1 : 0;
+    w.wring = ring + wv * D * RING_SLOT;
+    return w;
+}
+
+// DMA of tile j (r from src, q from ph when loadq) into its ring slot
+template <int D>
+__device__ __forceinline__ void ring_issue(const SpecTab& T, const RingWave& w, int j, const double* src,
+                                           const double* ph, bool loadq) {
+    const int lane = threadIdx.x & 63;
+    const int u = w.gw + j * w.W;
+    const int row = u / w.ntx, cx = u - row * w.ntx;
+    int kx = cx * 128 + 2 * lane;
+    if (kx >= T.Nx) kx = cx * 128;   // idle lanes fetch a valid address; never read
+    const int64_t i = (int64_t)row * T.Nx + kx;
+    double* slot = w.wring + (j % D) * RING_SLOT;
+    __builtin_amdgcn_global_load_lds((const void*)(src + i), (lds_void_t*)slot, 16, 0, 0);
+    if (loadq) __builtin_amdgcn_global_load_lds((const void*)(ph + i), (lds_void_t*)(slot + 128), 16, 0, 0);
+}
+
+// One pass over the wave's tiles: apply the planned steps of S0 (none for INIT), write r (and
+// q), accumulate the moments of the new state into acc.  issued: tiles [0, issued) already
+// have their DMAs in flight or landed (a prefetch), the rest of the prologue is issued here.
+template <int D, bool INIT>
+__device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, unsigned tab_a, const SStep& S0,
+                                          double* __restrict__ rh, double* __restrict__ ph,
+                                          const double* __restrict__ bh, double (&acc)[NACC], int issued) {
+    const int lane = threadIdx.x & 63;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
     const double c0 = INIT ? S0.gc0 : S0.c0, ic1 = 1.0 / (INIT ? S0.gc1 : S0.c1);
     const bool loadq = !INIT && k > 0;
-    const double* src = (INIT || k == 0) ? bh : rh;
-    // tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl)
-    double* tab = ring + RING_NW * D * RING_SLOT;
-    for (int i = threadIdx.x; i < T.Nx + T.Nt + T.nyl; i += S2_NTH)
-        tab[i] = (i < T.Nx) ? T.mx[i] : (i < T.Nx + T.Nt) ? T.mt[i - T.Nx] : T.my[T.y0 + i - T.Nx - T.Nt];
-    __syncthreads();
-    const unsigned tab_a = lds_u32(tab);
-
-    double acc[NACC];
-#pragma unroll
-    for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
+    const double* src = (INIT || k == 0) ? bh : rh;   // r_0 = b^ (the INIT pass leaves it there)
     auto moments = [&](double lam, double r, double q) {
         const double x = (lam - c0) * ic1, x2 = x + x;
         const double rr = r * r, rq = r * q, qq = q * q;
@@ -1666,39 +1742,18 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
             tm1 = t;
         }
     };
-
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int rows = T.Nt * T.nyl, ntx = (T.Nx + 127) / 128;
-    const int nwt = rows * ntx;
-    const int gw = blockIdx.x * RING_NW + w, W = gridDim.x * RING_NW;
-    const int nj = gw < nwt ? (nwt - 1 - gw) / W + 1 : 0;
-    double* wring = ring + w * D * RING_SLOT;
+    const int nj = w.nj;
     const int g = loadq ? 2 : 1;             // DMA instructions per tile
     constexpr int NS = INIT ? 1 : 2;         // store instructions per tile
-    auto tile_of = [&](int j, int& row, int& cx) {
-        const int u = gw + j * W;
-        row = u / ntx;
-        cx = u - row * ntx;
-    };
-    auto issue = [&](int j) {
-        int row, cx;
-        tile_of(j, row, cx);
-        int kx = cx * 128 + 2 * lane;
-        if (kx >= T.Nx) kx = cx * 128;   // idle lanes fetch a valid address; never read
-        const int64_t i = (int64_t)row * T.Nx + kx;
-        double* slot = wring + (j % D) * RING_SLOT;
-        __builtin_amdgcn_global_load_lds((const void*)(src + i), (lds_void_t*)slot, 16, 0, 0);
-        if (loadq) __builtin_amdgcn_global_load_lds((const void*)(ph + i), (lds_void_t*)(slot + 128), 16, 0, 0);
-    };
-    for (int j = 0; j < D - 1 && j < nj; ++j) issue(j);
+    for (int j = issued; j < D - 1 && j < nj; ++j) ring_issue<D>(T, w, j, src, ph, loadq);
     for (int j = 0; j < nj; ++j) {
-        if (j + D - 1 < nj) issue(j + D - 1);
+        if (j + D - 1 < nj) ring_issue<D>(T, w, j + D - 1, src, ph, loadq);
         const int nG = min(j + D - 1, nj - 1) - j, nS = min(j, D - 1);
         vm_wait(g * nG + NS * nS);
-        int row, cx;
-        tile_of(j, row, cx);
+        const int u = w.gw + j * w.W;
+        const int row = u / w.ntx, cx = u - row * w.ntx;
         const int kx = cx * 128 + 2 * lane;
-        const unsigned sa = lds_u32(wring + (j % D) * RING_SLOT) + 16 * lane;
+        const unsigned sa = lds_u32(w.wring + (j % D) * RING_SLOT) + 16 * lane;
         dbl2 rv = lds_ld128(sa);
         dbl2 qv = loadq ? lds_ld128(sa + 1024) : dbl2{0.0, 0.0};
         const int kt = row / T.nyl, ky = row - kt * T.nyl;
@@ -1716,16 +1771,19 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (INIT) {
             if (ok) *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
         } else {
-#pragma unroll
-            for (int s = 0; s < SMAX; ++s) {
-                if (s >= ns) break;
-                const double a = S0.a[s], b = S0.b[s];
-                const double p0 = (k + s == 0) ? r0 : fma(b, q0, r0);
-                const double p1 = (k + s == 0) ? r1 : fma(b, q1, r1);
-                r0 = fma(-a, l0 * p0, r0);
-                r1 = fma(-a, l1 * p1, r1);
-                q0 = p0;
-                q1 = p1;
+            // fully unrolled with a guard (not a break): a rolled loop would index S0.a / S0.b
+            // dynamically and put S0 in scratch (measured: 3x slower pass at SMAX 10)
+#pragma clang loop unroll(full)
+            for (int st = 0; st < SMAX; ++st) {
+                if (st < ns) {
+                    const double a = S0.a[st], b = S0.b[st];
+                    const double p0 = (k + st == 0) ? r0 : fma(b, q0, r0);
+                    const double p1 = (k + st == 0) ? r1 : fma(b, q1, r1);
+                    r0 = fma(-a, l0 * p0, r0);
+                    r1 = fma(-a, l1 * p1, r1);
+                    q0 = p0;
+                    q1 = p1;
+                }
             }
             if (ok) {
                 *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
@@ -1741,6 +1799,23 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
 #endif
         }
     }
+}
+
+template <int D, bool INIT, bool FUSE>
+__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_spec_s2r(
+        SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
+        RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
+    __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
+    const SStep S0 = *Sg;
+    if (!INIT && (S0.done || S0.nsteps == 0)) return;
+    double* tab = ring + RING_NW * D * RING_SLOT;
+    ring_stage_tables(T, tab);
+    __syncthreads();
+    double acc[NACC];
+#pragma unroll
+    for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
+    const RingWave w = ring_wave(T, ring, D);
+    ring_pass<D, INIT>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, 0);
     __shared__ double tot[NACC];
     if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
     if (!FUSE) {
@@ -1748,9 +1823,12 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
         return;
     }
     if (threadIdx.x >= 64) return;
-    __shared__ double xb[3 * NG + 2];
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
 }
+
+constexpr bool ring_fits(int D) { return (RING_NW * D * RING_SLOT + RING_TAB) * 8 <= 150 * 1024; }
+static_assert(ring_fits(FOTO_RING_D), "ring + tables exceed the LDS");
 
 // host launcher (D = 0: FOTO_RING_D)
 static hipError_t launch_s2_ring(const SpecTab& T, double* rh, double* ph, const double* bh, SStep* Sg, RedBuf rb,
@@ -1758,12 +1836,14 @@ static hipError_t launch_s2_ring(const SpecTab& T, double* rh, double* ph, const
                                  int nb = 256, hipStream_t s = 0) {
     if (D == 0) D = FOTO_RING_D;
 #define FOTO_RL(DD, I, F) k_spec_s2r<DD, I, F><<<nb, S2_NTH, 0, s>>>(T, rh, ph, bh, Sg, rb, rtol, maxiter, gath, rank)
-#define FOTO_RL_D(DD)                                                    \
-    if (D == DD) {                                                       \
-        if (init) { if (fuse) FOTO_RL(DD, true, true); else FOTO_RL(DD, true, false); } \
-        else { if (fuse) FOTO_RL(DD, false, true); else FOTO_RL(DD, false, false); }    \
+#define FOTO_RL_D(DD)                                                                        \
+    if (D == DD) {                                                                           \
+        if constexpr (ring_fits(DD)) {                                                       \
+            if (init) { if (fuse) FOTO_RL(DD, true, true); else FOTO_RL(DD, true, false); } \
+            else { if (fuse) FOTO_RL(DD, false, true); else FOTO_RL(DD, false, false); }    \
+        } else return hipErrorInvalidValue;                                                  \
     }
-    FOTO_RL_D(2) else FOTO_RL_D(3) else FOTO_RL_D(4) else return hipErrorInvalidValue;
+    FOTO_RL_D(2) else FOTO_RL_D(3) else FOTO_RL_D(4) else FOTO_RL_D(5) else FOTO_RL_D(8) else return hipErrorInvalidValue;
 #undef FOTO_RL_D
 #undef FOTO_RL
     return hipGetLastError();
@@ -1781,7 +1861,7 @@ __global__ __launch_bounds__(64) void k_spec_s2_plan(SStep* Sg, const double* __
     }
     __syncthreads();
     if (!init && S0.done) return;
-    __shared__ double xb[3 * NG + 2];
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, init, rtol, maxiter);
 }
 
@@ -1859,7 +1939,7 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
     for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
     __syncthreads();
     if (threadIdx.x >= 64) return;
-    __shared__ double xb[3 * NG + 2];
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
 }
 

@@ -61,6 +61,7 @@ int main() {
         (void)hipMemcpy(Sg, &S0, sizeof(SStep), hipMemcpyHostToDevice);
         (void)hipMemcpy(Sg2, &S0, sizeof(SStep), hipMemcpyHostToDevice);
     };
+    printf("SMAX=%d S2_NTH=%d ring D=%d\n", SMAX, S2_NTH, FOTO_RING_D);
     // correctness: one pass each from the same state, moments to gath (no fused plan)
     reset();
     const int G = 256;
@@ -107,12 +108,12 @@ int main() {
     timeit("pure stream r,q (1024 x 256)", [&] { stream_rq<<<1024, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
     timeit("pure stream r,q (2048 x 256)", [&] { stream_rq<<<2048, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
     timeit("product k_spec_s2, moments only", [&] { k_spec_s2<true, false, false><<<256, S2_NTH>>>(T, r, p, b, Sg, rb, 1e-6, 1000, gath, 0); });
-    for (int d : {2, 3, 4}) {
+    for (int d : {2, 4, FOTO_RING_D}) {
         char nm[64];
         snprintf(nm, sizeof nm, "ring D=%d, moments only", d);
         timeit(nm, [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, false, false, d); });
     }
-    timeit("ring INIT, moments only", [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, true, false, 4); });
+    timeit("ring INIT, moments only", [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, true, false, 0); });
     timeit("product INIT, moments only", [&] { k_spec_s2<true, true, false><<<256, S2_NTH>>>(T, r, p, b, Sg, rb, 1e-6, 1000, gath, 0); });
     auto single = [&](const char* name, auto launch) {
         float best = 1e9;
@@ -128,7 +129,7 @@ int main() {
         }
         printf("%-44s %6.1f us (single launch)\n", name, best * 1e3);
     };
-    single("ring D=4 moments only", [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, false, false, 4); });
+    single("ring D=4 moments only", [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, false, false, 0); });
     single("plan kernel alone (8 steps)", [&] { k_spec_s2_plan<<<1, 64>>>(Sg2, gath2, 1, 0, 1e-6, 1000); });
     single("plan kernel alone (maxiter 0)", [&] { k_spec_s2_plan<<<1, 64>>>(Sg2, gath2, 1, 0, 1e-6, 0); });
     {
@@ -144,7 +145,7 @@ int main() {
         for (int rep = 0; rep < 20; ++rep) {
             (void)hipMemcpy(Sg2, &S0, sizeof(SStep), hipMemcpyHostToDevice);
             (void)hipEventRecord(e0);
-            (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, nullptr, 0, false, true, 4);
+            (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, nullptr, 0, false, true, 0);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float t;
