@@ -66,6 +66,10 @@ int check2(int Nx, int Ny) {
         set_error("image %dx%d: every axis needs >= 2 points", Nx, Ny);
         return FOTO_ERR_ARG;
     }
+    if ((int64_t)Nx * Ny >= ((int64_t)1 << 31)) {   // pixel indices are 32-bit in the kernels
+        set_error("image %dx%d: more than 2^31 pixels", Nx, Ny);
+        return FOTO_ERR_ARG;
+    }
     return 0;
 }
 

@@ -10,6 +10,8 @@
 // with the same last-block reductions as the BB CG.
 #include "foto_internal.h"
 
+#include <algorithm>
+
 namespace foto {
 
 // reductions shared with foto_kernels.hip (re-declared here: header-only templates)
@@ -73,6 +75,22 @@ __device__ bool gn_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
     return true;
 }
 
+// PCG kernels run a grid-stride loop over pixels on at most two blocks per CU: each block
+// adds one agent-scope ticket per launch, and 1200 tickets on one address (one block per
+// 256 pixels at 640x480) serialised at the memory side (~28 us per kernel, rocprofv3); with
+// 512 blocks and a 512-entry gather the kernels are bandwidth-bound.
+static int gn_grid(int64_t n) {
+    static int cap = 0;
+    if (cap == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        cap = 2 * cus;
+    }
+    return (int)std::min<int64_t>(flat_blocks(n), cap);
+}
+
 // ----------------------------------------------------------------------------- coefficients
 
 // classical.py:90-100
@@ -121,23 +139,29 @@ struct GNPix {
 
 __device__ __forceinline__ GNPix gn_pix(int w, int h, int64_t i) {
     GNPix P;
-    P.y = (int)(i / w);
-    P.x = (int)(i - (int64_t)P.y * w);
+    // 32-bit division (w h < 2^31): the 64-bit one is a long software sequence per pixel
+    P.y = (int)((unsigned)i / (unsigned)w);
+    P.x = (int)i - P.y * w;
     P.hy = P.y > 0; P.hY = P.y < h - 1; P.hx = P.x > 0; P.hX = P.x < w - 1;
     P.c = (double)((int)P.hy + (int)P.hY + (int)P.hx + (int)P.hX);
     return P;
 }
 
 // one field's Laplacian block row in CSR order: (y-1), (x-1), diag, (x+1), (y+1)
+// The five values are fetched unconditionally (clamped indices) and the missing neighbours
+// skipped by selects: with the fetches behind branches every neighbour was its own memory
+// round trip (~25 us per PCG kernel at 640x480).  Same additions in the same order.
 template <class F>
 __device__ __forceinline__ double gn_lap_row(const GNPix& P, int w, int64_t i, double coef, double dg, F val,
                                              double s) {
     const double m = -coef;
-    if (P.hy) s += m * val(i - w);
-    if (P.hx) s += m * val(i - 1);
-    s += dg * val(i);
-    if (P.hX) s += m * val(i + 1);
-    if (P.hY) s += m * val(i + w);
+    const double vym = val(P.hy ? i - w : i), vxm = val(P.hx ? i - 1 : i), vc = val(i);
+    const double vxp = val(P.hX ? i + 1 : i), vyp = val(P.hY ? i + w : i);
+    s = P.hy ? s + m * vym : s;
+    s = P.hx ? s + m * vxm : s;
+    s += dg * vc;
+    s = P.hX ? s + m * vxp : s;
+    s = P.hY ? s + m * vyp : s;
     return s;
 }
 
@@ -209,17 +233,16 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_init(int w, int h, const double* 
                                                     double* __restrict__ r, double* __restrict__ z, RedBuf rb,
                                                     double* gath) {
     const int64_t n = (int64_t)w * h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
     double rr = 0.0, rz = 0.0;
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
         const GNPix P = gn_pix(w, h, i);
         const double ru = b[i], rv = b[n + i], rm = b[2 * n + i];
         r[i] = ru; r[n + i] = rv; r[2 * n + i] = rm;
         double zu, zv, zm;
         gn_precond(P.c, fx[i], fy[i], f2[i], a, l, ru, rv, rm, zu, zv, zm);
         z[i] = zu; z[n + i] = zv; z[2 * n + i] = zm;
-        rr = ru * ru + rv * rv + rm * rm;
-        rz = ru * zu + rv * zv + rm * zm;
+        rr += ru * ru + rv * rv + rm * rm;
+        rz += ru * zu + rv * zv + rm * zm;
     }
     double v[2] = {rr, rz}, tot[2];
     if (gn_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) { gath[0] = tot[0]; gath[1] = tot[1]; }
@@ -228,7 +251,7 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_init(int w, int h, const double* 
 hipError_t launch_gn_pcg_init(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
                               double lam, const double* b, double* r, double* z, RedBuf rb, double* gath,
                               hipStream_t s) {
-    k_gn_pcg_init<<<flat_blocks((int64_t)w * h), NT, 0, s>>>(w, h, fx, fy, f2, alpha, lam, b, r, z, rb, gath);
+    k_gn_pcg_init<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, fx, fy, f2, alpha, lam, b, r, z, rb, gath);
     return hipGetLastError();
 }
 
@@ -250,9 +273,8 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_dir(int w, int h, int k, const do
     }
     const double beta = (k > 0) ? rz / S->rho : 0.0;
     const int64_t n = (int64_t)w * h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
     double pq = 0.0;
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
         const GNPix P = gn_pix(w, h, i);
         auto pv = [&](int f, int64_t j) -> double {
             const int64_t o = f * n + j;
@@ -262,7 +284,7 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_dir(int w, int h, int k, const do
         gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, pv, qu, qv, qm);
         const double pu = pv(0, i), pvv = pv(1, i), pm = pv(2, i);
         pn[i] = pu; pn[n + i] = pvv; pn[2 * n + i] = pm;
-        pq = pu * qu + pvv * qv + pm * qm;
+        pq += pu * qu + pvv * qv + pm * qm;
     }
     double v[1] = {pq}, tot[1];
     if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) {
@@ -275,7 +297,7 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_dir(int w, int h, int k, const do
 hipError_t launch_gn_pcg_dir(int w, int h, int k, const double* fx, const double* fy, const double* f2, double alpha,
                              double lam, const double* z, const double* pold, double* pnew, CGScal* S, RedBuf rb,
                              const double* gath_rz, double* gath_pq, double rtol, hipStream_t s) {
-    k_gn_pcg_dir<<<flat_blocks((int64_t)w * h), NT, 0, s>>>(w, h, k, fx, fy, f2, alpha, lam, z, pold, pnew, S, rb,
+    k_gn_pcg_dir<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, k, fx, fy, f2, alpha, lam, z, pold, pnew, S, rb,
                                                             gath_rz, gath_pq, rtol);
     return hipGetLastError();
 }
@@ -290,9 +312,8 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_upd(int w, int h, int k, const do
     if (S->done) return;
     const double alpha = S->rho / gath_pq[0];
     const int64_t n = (int64_t)w * h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
     double rr = 0.0, rz = 0.0;
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
         const GNPix P = gn_pix(w, h, i);
         const double cfx = fx[i], cfy = fy[i], cf2 = f2[i];
         double qu, qv, qm;
@@ -310,17 +331,20 @@ __global__ __launch_bounds__(NT) void k_gn_pcg_upd(int w, int h, int k, const do
         double zu, zv, zm;
         gn_precond(P.c, cfx, cfy, cf2, a, l, rn[0], rn[1], rn[2], zu, zv, zm);
         z[i] = zu; z[n + i] = zv; z[2 * n + i] = zm;
-        rr = rn[0] * rn[0] + rn[1] * rn[1] + rn[2] * rn[2];
-        rz = rn[0] * zu + rn[1] * zv + rn[2] * zm;
+        rr += rn[0] * rn[0] + rn[1] * rn[1] + rn[2] * rn[2];
+        rz += rn[0] * zu + rn[1] * zv + rn[2] * zm;
     }
     double v[2] = {rr, rz}, tot[2];
-    if (gn_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) { gath_rz[0] = tot[0]; gath_rz[1] = tot[1]; }
+    if (gn_reduce_last<2>(v, rb, tot) && threadIdx.x == 0) {
+        gath_rz[0] = tot[0];
+        gath_rz[1] = tot[1];
+    }
 }
 
 hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double* fy, const double* f2, double alpha,
                              double lam, const double* p, double* x, double* r, double* z, CGScal* S, RedBuf rb,
                              const double* gath_pq, double* gath_rz, hipStream_t s) {
-    k_gn_pcg_upd<<<flat_blocks((int64_t)w * h), NT, 0, s>>>(w, h, k, fx, fy, f2, alpha, lam, p, x, r, z, S, rb,
+    k_gn_pcg_upd<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, k, fx, fy, f2, alpha, lam, p, x, r, z, S, rb,
                                                             gath_pq, gath_rz);
     return hipGetLastError();
 }
