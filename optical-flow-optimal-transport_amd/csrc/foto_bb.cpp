@@ -431,10 +431,10 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
         const double nv = (double)s.g.nloc * (double)s.g.nxy;
         hipEvent_t e = c->kt.start(c->s);
         FOTO_HIP_CHECK(launch_rhs(s.g, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], s.rho0, s.rhoT, c->r,
-                                  s.rv, s.rb, s.gath_rr(), s.rank, c->s));
+                                  s.rv, s.rb, c->o.cg_mode == 0 ? s.gath_rr() : nullptr, s.rank, c->s));
         c->kt.stop(e, c->s, FOTO_K_RHS, 56.0 * nv);
     }
-    FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
     // phase boundaries are recorded, not waited on: the one host wait per outer iteration
     // is the crit readback below (a wait here idled the GPU for the host's wake-up)
     FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));

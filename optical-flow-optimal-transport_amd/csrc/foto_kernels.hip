@@ -438,6 +438,7 @@ __global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mu
             tp = tpp;
         }
     }
+    if (!gath) return;   // F.F only feeds the stencil CG's stopping rule (the spectral CG takes it from b^)
     double v[1] = {ff}, tot[1];
     if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
 }

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Outer iterations/s of the Benamou-Brenier solve on one GPU at the SURVEY.md §8 config sizes
+(synthetic translating-Gaussian pairs; r = 1, eps = 1e-2, stop rules off).
+usage: python tools/size_sweep.py [NxxNyxNt ...]"""
+import sys
+import time
+
+sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "..",
+                                              "optical-flow-optimal-transport_amd"))
+from foto.bb import BBSolver  # noqa: E402
+from foto.synthetic import translating_gaussian  # noqa: E402
+
+sizes = sys.argv[1:] or ["64x64x8", "584x388x32", "640x480x32", "1024x1024x64"]
+for sz in sizes:
+    Nx, Ny, Nt = (int(v) for v in sz.split("x"))
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, device=0, cg_mode=2) as s:
+        s.iterate(2, 0.0, stop_rules=False)
+        s.sync()
+        k = 5
+        t = time.perf_counter()
+        s.iterate(k, 0.0, stop_rules=False)
+        s.sync()
+        dt = time.perf_counter() - t
+        its = s.cg_its[-k:]
+        print(f"{sz}: {k / dt:8.2f} outer it/s, {1e3 * dt / k:8.3f} ms/outer, CG its {its}", flush=True)
