@@ -1192,7 +1192,8 @@ struct SStep {
     double rho_prev;   // rho_{k-1}
     double atol;
     double c0, c1;     // Chebyshev interval of the next pass's moments: lam in [c0 - c1, c0 + c1]
-    double gc0, gc1;   // the whole spectrum's interval (fixed; every solve's INIT moments use it)
+    double gc0, gc1;   // the whole spectrum's interval (fixed)
+    double ic0, ic1;   // interval of the next solve's INIT moments (set by each INIT plan)
 };
 
 // Interval adaptation: the Chebyshev-Krylov basis is well conditioned when [c0 - c1, c0 + c1]
@@ -1205,6 +1206,7 @@ struct SStep {
 // grid 24 -> 22 passes on the first outer iteration, 33 -> 28 at 160x120x32; no change in
 // CG counts or iterates.
 constexpr double S_KAPPA = 2.0;
+constexpr int S_PROJ = (NMOM - 3) / 2;   // projected interval after n <= S_PROJ steps (2n + 2 < NMOM)
 
 // Plan helpers.  Coefficient vectors are distributed one entry per lane: lane j < NG holds
 // index j of (r part | q part), lanes >= NG hold 0; lane j also holds row j of the Gram
@@ -1372,8 +1374,8 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
                                 double rtol, int maxiter) {
     const int lane = threadIdx.x & 63;
     if (init) {
-        S.c0 = S.gc0;   // the INIT moments were taken over the whole spectrum
-        S.c1 = S.gc1;
+        S.c0 = S.ic0;   // the interval the INIT moments were taken over
+        S.c1 = S.ic1;
         S.k = 0;
         S.rho_prev = 0.0;
         S.atol = fmax(0.0, rtol * sqrt(tot[0]));   // scipy: max(atol, rtol * ||b||)
@@ -1455,23 +1457,54 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         S.iters = conv ? S.k + n : maxiter;
         if (n == 0) S.done = conv ? 1 : 2;   // nothing left to apply
     }
-    // next pass's interval, from the measure of the state these moments describe
-    double nc0 = S.c0, nc1 = S.c1;
-    if (tot[0] > 0.0) {
-        const double ex = tot[1] / tot[0], ex2 = 0.5 * (tot[2] + tot[0]) / tot[0];
-        const double mean = S.c0 + S.c1 * ex, sd = S.c1 * sqrt(fmax(ex2 - ex * ex, 0.0));
-        const double lmin = S.gc0 - S.gc1, lmax = S.gc0 + S.gc1;
-        double hi = fmin(lmax, mean + S_KAPPA * sd);
+    // Next pass's interval.  After n <= S_PROJ steps the plan knows the new residual's
+    // coefficients R, so the mean and variance of its measure are Gram forms
+    // (<R, lam R>, <lam R, lam R> over <R, R>; degrees <= 2n + 2 < NMOM); after more steps
+    // it falls back to the measure these moments describe (one pass behind).  An INIT plan
+    // also sets the next solve's INIT interval from the measure of b^ (consecutive outer
+    // iterations' right-hand sides are close).
+    const double lmin = S.gc0 - S.gc1, lmax = S.gc0 + S.gc1;
+    auto to_interval = [&](double mean, double var, double& c0o, double& c1o) {
+        double hi = fmin(lmax, mean + S_KAPPA * sqrt(fmax(var, 0.0)));
         hi = fmax(hi, lmin + 1e-3 * (lmax - lmin));
         if (hi == hi) {   // not NaN
-            nc0 = 0.5 * (hi + lmin);
-            nc1 = 0.5 * (hi - lmin);
+            c0o = 0.5 * (hi + lmin);
+            c1o = 0.5 * (hi - lmin);
+        }
+    };
+    double nc0 = S.c0, nc1 = S.c1, ic0 = S.ic0, ic1 = S.ic1;
+    double mom_mean = 0.0, mom_var = -1.0;   // the moments' own measure
+    if (tot[0] > 0.0) {
+        const double ex = tot[1] / tot[0], ex2 = 0.5 * (tot[2] + tot[0]) / tot[0];
+        mom_mean = S.c0 + S.c1 * ex;
+        mom_var = S.c1 * S.c1 * (ex2 - ex * ex);
+    }
+    if (init && mom_var >= 0.0) to_interval(mom_mean, mom_var, ic0, ic1);
+    bool projected = false;
+    if (n > 0 && n <= S_PROJ && !S.fin) {
+        double c1r, c2r, c3r;
+#if FOTO_PLAN_DPP
+        const double LR = plan_mul_lam_dpp(R, S.c0, S.c1);
+        const double rr = plan_ip_dpp(R, R, hrow, &c1r, n + 1);
+        const double rl = plan_ip_dpp(R, LR, hrow, &c2r, n + 2);
+        const double ll = plan_ip_dpp(LR, LR, hrow, &c3r, n + 2);
+#else
+        const double LR = plan_mul_lam(R, S.c0, S.c1, xb);
+        const double rr = plan_ip(R, R, hrow, xb, &c1r);
+        const double rl = plan_ip(R, LR, hrow, xb, &c2r);
+        const double ll = plan_ip(LR, LR, hrow, xb, &c3r);
+#endif
+        if (rr > 0.0) {
+            const double mean = rl / rr;
+            to_interval(mean, ll / rr - mean * mean, nc0, nc1);
+            projected = true;
         }
     }
+    if (!projected && mom_var >= 0.0) to_interval(mom_mean, mom_var, nc0, nc1);
     if (lane == 0) {   // scalars only: a[], b[] were stored above
         Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
         Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
-        Sg->c0 = nc0; Sg->c1 = nc1;
+        Sg->c0 = nc0; Sg->c1 = nc1; Sg->ic0 = ic0; Sg->ic1 = ic1;
     }
 }
 
@@ -1526,7 +1559,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
     const SStep S0 = *Sg;             // uniform: scalar loads
     if (!INIT && (S0.done || S0.nsteps == 0)) return;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
-    const double c0 = INIT ? S0.gc0 : S0.c0, ic1 = 1.0 / (INIT ? S0.gc1 : S0.c1);
+    const double c0 = INIT ? S0.ic0 : S0.c0, ic1 = 1.0 / (INIT ? S0.ic1 : S0.c1);
     const bool loadq = !INIT && k > 0;
     // r_0 = b^: the INIT pass (or the fused t-axis kernel, which writes no r^) leaves it in b^
     const double* src = (INIT || k == 0) ? bh : rh;
@@ -1719,7 +1752,7 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
                                           const double* __restrict__ bh, double (&acc)[NACC], int issued) {
     const int lane = threadIdx.x & 63;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
-    const double c0 = INIT ? S0.gc0 : S0.c0, ic1 = 1.0 / (INIT ? S0.gc1 : S0.c1);
+    const double c0 = INIT ? S0.ic0 : S0.c0, ic1 = 1.0 / (INIT ? S0.ic1 : S0.c1);
     const bool loadq = !INIT && k > 0;
     const double* src = (INIT || k == 0) ? bh : rh;   // r_0 = b^ (the INIT pass leaves it there)
     auto moments = [&](double lam, double r, double q) {
@@ -1894,7 +1927,7 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
     const int64_t ncols = (int64_t)T.nyl * T.Nx;
     const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
     const SStep S0 = *Sg;
-    const double c0 = S0.gc0, ic1 = 1.0 / S0.gc1;   // INIT: the whole spectrum
+    const double c0 = S0.ic0, ic1 = 1.0 / S0.ic1;   // INIT interval (previous solve's b^ measure)
     double acc[NMOM];
 #pragma unroll
     for (int m = 0; m < NMOM; ++m) acc[m] = 0.0;
@@ -2297,6 +2330,8 @@ static int reset_s2(SpecImpl* P, hipStream_t s) {
     h.c1 = P->c1;
     h.gc0 = P->c0;
     h.gc1 = P->c1;
+    h.ic0 = P->c0;   // the first solve's INIT moments: the whole spectrum
+    h.ic1 = P->c1;
     *P->hS2 = h;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->S2, P->hS2, sizeof(SStep), hipMemcpyHostToDevice, s));
     FOTO_HIP_CHECK(hipStreamSynchronize(s));   // hS2 is reused by polling

@@ -4,8 +4,9 @@ csrc/foto_spectral.hip runs scipy's CG recurrence (benamou_brenier.py:85 ->
 scipy.sparse.linalg.cg) in the DCT eigenbasis, where A = C^T diag(lam) C and every CG
 update is pointwise.  One pass applies up to SMAX = 8 iterations whose scalars were planned
 from Chebyshev moments of the pass-start state (r_k, p_{k-1}) over an interval adapted to
-the residual measure (whole spectrum at INIT, then [lmin, mean + 2 sd] of the previous
-pass's measure); step i > 0 is taken only
+the residual measure ([lmin, mean + 2 sd]: of b^ of the previous solve for the INIT moments,
+the whole spectrum for a run's first solve; of the new residual, projected through the Gram,
+after short passes; of the pass-start state otherwise); step i > 0 is taken only
 while its two Gram-form inner products have cancellation ratio sum|terms| / |value| <=
 S_CLIM = 1e4, and the moments are summed with compensated block reductions (correctly
 rounded to ~1 ulp).  This module restates that rule on the CPU (test infrastructure: the
@@ -29,6 +30,7 @@ NMOM = 2 * SMAX
 NCO = SMAX + 1
 S_CLIM = 1e4
 S_KAPPA = 2.0
+S_PROJ = (NMOM - 3) // 2   # projected interval after n <= S_PROJ steps
 
 
 def _lam(Nt, Ny, Nx, r, eps):
@@ -82,7 +84,7 @@ def _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter):
             if not cr <= S_CLIM:
                 break
         if rho == 0 or math.sqrt(rho) < atol:
-            return al, be, True, rho_prev
+            return al, be, True, rho_prev, None
         beta = 0.0 if k + i == 0 else rho / rho_prev
         Pn = R.copy() if k + i == 0 else beta * P + R
         Q = mul_lam(Pn)
@@ -95,25 +97,39 @@ def _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter):
         rho_prev = rho
         al.append(alpha)
         be.append(beta)
-    return al, be, False, rho_prev
+    proj = None
+    if 0 < len(al) <= S_PROJ:   # mean / variance of the new residual's measure from the Gram
+        LR = mul_lam(R)
+        rr_, _ = ip(R, R)
+        if rr_ > 0:
+            mean = ip(R, LR)[0] / rr_
+            proj = (mean, ip(LR, LR)[0] / rr_ - mean * mean)
+    return al, be, False, rho_prev, proj
 
 
-def _next_interval(Mrr, c0, c1, lmin, lmax):
-    """Next pass's Chebyshev interval [lmin, min(lmax, mean + S_KAPPA sd)] of the residual
-    measure the moments describe (csrc/foto_spectral.hip sstep_plan_wave)."""
+def _interval(mean, var, c0, c1, lmin, lmax):
+    """Chebyshev interval [lmin, min(lmax, mean + S_KAPPA sd)] (csrc/foto_spectral.hip)."""
+    hi = max(min(lmax, mean + S_KAPPA * math.sqrt(max(var, 0.0))), lmin + 1e-3 * (lmax - lmin))
+    return (0.5 * (hi + lmin), 0.5 * (hi - lmin)) if hi == hi else (c0, c1)
+
+
+def _moment_stats(Mrr, c0, c1):
+    """Mean and variance of the measure the rr moments describe (None if empty)."""
     if not Mrr[0] > 0:
-        return c0, c1
+        return None
     ex, ex2 = Mrr[1] / Mrr[0], 0.5 * (Mrr[2] + Mrr[0]) / Mrr[0]
-    mean, sd = c0 + c1 * ex, c1 * math.sqrt(max(ex2 - ex * ex, 0.0))
-    hi = max(min(lmax, mean + S_KAPPA * sd), lmin + 1e-3 * (lmax - lmin))
-    return 0.5 * (hi + lmin), 0.5 * (hi - lmin)
+    return c0 + c1 * ex, c1 * c1 * (ex2 - ex * ex)
 
 
-def sstep_cg(b, Nt, Ny, Nx, r, eps, rtol=1e-6, maxiter=1000, stats=None):
-    """x, info, iterations -- scipy's contract (x0 = 0, M = I)."""
+def sstep_cg(b, Nt, Ny, Nx, r, eps, rtol=1e-6, maxiter=1000, stats=None, carry=None):
+    """x, info, iterations -- scipy's contract (x0 = 0, M = I).  carry: dict kept across the
+    solves of one Benamou-Brenier run (the INIT interval comes from the previous solve's b^)."""
     lam = _lam(Nt, Ny, Nx, r, eps)
     lmin, lmax = lam.min(), lam.max()   # r eps, r eps + r (mu_t + mu_y + mu_x)_max
-    c0, c1 = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)   # INIT: the whole spectrum
+    c0, c1 = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)   # the first solve's INIT: the whole spectrum
+    if carry is not None and "init" in carry:
+        c0, c1 = carry["init"]
+    first = True
     bh = sfft.dctn(b.reshape(Nt, Ny, Nx), norm="ortho").ravel()
     rr, q = bh.copy(), np.zeros_like(bh)
     atol = max(0.0, rtol * math.sqrt(math.fsum(bh * bh)))
@@ -126,9 +142,16 @@ def sstep_cg(b, Nt, Ny, Nx, r, eps, rtol=1e-6, maxiter=1000, stats=None):
         for m in range(2, NMOM):
             T[m] = 2 * x * T[m - 1] - T[m - 2]
         Mrr, Mrq, Mqq = _moments(T, rr * rr), _moments(T, rr * q), _moments(T, q * q)
-        al, be, conv, rho_prev = _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter)
+        al, be, conv, rho_prev, proj = _plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter)
         passes += 1
-        c0, c1 = _next_interval(Mrr, c0, c1, lmin, lmax)
+        ms = _moment_stats(Mrr, c0, c1)
+        if first and carry is not None and ms is not None:
+            carry["init"] = _interval(*ms, c0, c1, lmin, lmax)
+        first = False
+        if proj is not None:
+            c0, c1 = _interval(*proj, c0, c1, lmin, lmax)
+        elif ms is not None:
+            c0, c1 = _interval(*ms, c0, c1, lmin, lmax)
         for a, bt in zip(al, be):
             p = rr.copy() if k == 0 else bt * q + rr
             rr = rr - a * (lam * p)
@@ -162,7 +185,9 @@ def test_sstep_plan_golden_solves(gold, name, monkeypatch):
     Nt, Ny, Nx = (int(s) for s in d["shape"])
     r, tol, eps, max_it = d["params"]
     stats = {}
-    monkeypatch.setattr(O, "cg", lambda mv, b, rtol=1e-6, maxiter=1000: sstep_cg(b, Nt, Ny, Nx, r, eps, rtol, maxiter, stats))
+    carry = {}
+    monkeypatch.setattr(O, "cg", lambda mv, b, rtol=1e-6, maxiter=1000: sstep_cg(b, Nt, Ny, Nx, r, eps, rtol, maxiter, stats,
+                                                                                 carry))
     st = {}
     u, v, m = O.solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r, tol, eps, int(max_it), log=lambda *a: None, stats=st)
     assert len(st["crit"]) == len(d["crit"])
