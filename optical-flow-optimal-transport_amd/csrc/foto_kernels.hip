@@ -29,21 +29,21 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Fixed-tree block sum of K values; result valid in thread 0.  `sh` holds K*NT/64 doubles.
-template <int K>
+template <int K, int NTH = NT>
 __device__ __forceinline__ void block_sum(double (&v)[K], double* sh) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         v[k] = wave_sum(v[k]);
-        if (lane == 0) sh[k * (NT / 64) + w] = v[k];
+        if (lane == 0) sh[k * (NTH / 64) + w] = v[k];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            double s = sh[k * (NT / 64)];
+            double s = sh[k * (NTH / 64)];
 #pragma unroll
-            for (int j = 1; j < NT / 64; ++j) s += sh[k * (NT / 64) + j];
+            for (int j = 1; j < NTH / 64; ++j) s += sh[k * (NTH / 64) + j];
             v[k] = s;
         }
     }
@@ -53,11 +53,11 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* sh) {
 // partials in block order (deterministic) and returns true with the totals in thread 0.
 // Hand-off: partials stored sc1 (write-through) + vmcnt(0) before an agent-scope ticket
 // add; the last block reads them with sc1 loads after its add returned and a barrier.
-template <int K>
+template <int K, int NTH = NT>
 __device__ bool grid_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
-    __shared__ double sh[K * (NT / 64)];
+    __shared__ double sh[K * (NTH / 64)];
     __shared__ int is_last;
-    block_sum<K>(v, sh);
+    block_sum<K, NTH>(v, sh);
     const int nb = gridDim.x;
     if (threadIdx.x == 0) {
 #pragma unroll
@@ -73,12 +73,12 @@ __device__ bool grid_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    for (int i = threadIdx.x; i < nb; i += NT) {
+    for (int i = threadIdx.x; i < nb; i += NTH) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
             acc[k] += __hip_atomic_load(&rb.partials[(int64_t)k * nb + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    block_sum<K>(acc, sh);
+    block_sum<K, NTH>(acc, sh);
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) tot[k] = acc[k];
@@ -400,7 +400,12 @@ hipError_t launch_div_st(const Geo& g, const double* wt, const double* wx, const
 
 // F = div_st(mu - r q); F[t=0] -= rho0 - rho[0] + r a[0]; F[t=Nt-1] += rhoT - rho + r a
 // (benamou_brenier.py:64-82, dt = 1).  F.F partial -> gath[rank] (= b.b for CG).
-__global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mut, const double* __restrict__ mux,
+#ifndef FOTO_RHS_TY
+#define FOTO_RHS_TY 2
+#endif
+constexpr int RHS_TY = FOTO_RHS_TY;    // rows per block: the y-neighbour rows a tile re-reads are 2 / RHS_TY extra
+constexpr int RHS_NT = TX * RHS_TY;
+__global__ __launch_bounds__(RHS_NT) void k_rhs(Geo g, const double* __restrict__ mut, const double* __restrict__ mux,
                                             const double* __restrict__ muy, const double* __restrict__ qt,
                                             const double* __restrict__ qx, const double* __restrict__ qy,
                                             const double* __restrict__ rho0, const double* __restrict__ rhoT,
@@ -410,7 +415,7 @@ __global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mu
     // ahead), the x / y fields' neighbours are same-row / adjacent-row loads (L1 / L2 hits).
     const int ntx = (g.Nx + TX - 1) / TX;
     const int x = (blockIdx.x % ntx) * TX + (threadIdx.x & (TX - 1));
-    const int y = (blockIdx.x / ntx) * TY + threadIdx.x / TX;
+    const int y = (blockIdx.x / ntx) * RHS_TY + threadIdx.x / TX;
     const bool in = x < g.Nx && y < g.Ny;
     const int64_t nxy = g.nxy, off = in ? (int64_t)y * g.Nx + x : 0;
     const bool has_lo = g.t0 > 0, has_hi = g.t0 + g.nloc < g.Nt;
@@ -440,13 +445,14 @@ __global__ __launch_bounds__(NT) void k_rhs(Geo g, const double* __restrict__ mu
     }
     if (!gath) return;   // F.F only feeds the stencil CG's stopping rule (the spectral CG takes it from b^)
     double v[1] = {ff}, tot[1];
-    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
+    if (grid_reduce_last<1, RHS_NT>(v, rb, tot) && threadIdx.x == 0) gath[rank] = tot[0];
 }
 
 hipError_t launch_rhs(const Geo& g, const double* mut, const double* mux, const double* muy, const double* qt,
                       const double* qx, const double* qy, const double* rho0, const double* rhoT, double r,
                       double* F, RedBuf rb, double* gath, int rank, hipStream_t s) {
-    k_rhs<<<march_blocks(g), NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb, gath, rank);
+    const int nb = ((g.Nx + TX - 1) / TX) * ((g.Ny + RHS_TY - 1) / RHS_TY);
+    k_rhs<<<nb, RHS_NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb, gath, rank);
     return hipGetLastError();
 }
 
