@@ -1187,7 +1187,7 @@ struct SStep {
     int done;     // 1 converged, 2 maxiter reached (host polls this)
     int iters;    // iterations at finish
     int passes;   // plans made in this solve
-    int pad;
+    int flags;    // bit 0: no interval adaptation (A/B runs, FOTO_SADAPT=0)
     double a[SMAX], b[SMAX];
     double rho_prev;   // rho_{k-1}
     double atol;
@@ -1479,9 +1479,10 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         mom_mean = S.c0 + S.c1 * ex;
         mom_var = S.c1 * S.c1 * (ex2 - ex * ex);
     }
-    if (init && mom_var >= 0.0) to_interval(mom_mean, mom_var, ic0, ic1);
+    const bool adapt = !(S.flags & 1);
+    if (adapt && init && mom_var >= 0.0) to_interval(mom_mean, mom_var, ic0, ic1);
     bool projected = false;
-    if (n > 0 && n <= S_PROJ && !S.fin) {
+    if (adapt && n > 0 && n <= S_PROJ && !S.fin) {
         double c1r, c2r, c3r;
 #if FOTO_PLAN_DPP
         const double LR = plan_mul_lam_dpp(R, S.c0, S.c1);
@@ -1500,7 +1501,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
             projected = true;
         }
     }
-    if (!projected && mom_var >= 0.0) to_interval(mom_mean, mom_var, nc0, nc1);
+    if (adapt && !projected && mom_var >= 0.0) to_interval(mom_mean, mom_var, nc0, nc1);
     if (lane == 0) {   // scalars only: a[], b[] were stored above
         Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
         Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
@@ -2332,6 +2333,10 @@ static int reset_s2(SpecImpl* P, hipStream_t s) {
     h.gc1 = P->c1;
     h.ic0 = P->c0;   // the first solve's INIT moments: the whole spectrum
     h.ic1 = P->c1;
+    {
+        const char* e = getenv("FOTO_SADAPT");   // 0: whole-spectrum interval for every pass (A/B runs)
+        h.flags = (e && atoi(e) == 0) ? 1 : 0;
+    }
     *P->hS2 = h;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->S2, P->hS2, sizeof(SStep), hipMemcpyHostToDevice, s));
     FOTO_HIP_CHECK(hipStreamSynchronize(s));   // hS2 is reused by polling
