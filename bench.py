@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """FOTO hot-path benchmark: Benamou-Brenier outer iterations/s on the 640x480x32 grid.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1|2] [--no-cpu-baseline] [--no-gn]
 
 A "step" is one outer iteration of benamou_brenier.solve (benamou_brenier.py:204-258:
 RHS + CG Poisson solve + stepB/stepC + criterion) over the synthetic 640x480x32
@@ -10,6 +10,10 @@ parameters), with every input and all solver state resident in HBM.  The stop ru
 disabled so exactly K steps run.  With N > 1 (torch.distributed.run, one process per GPU)
 the time axis is sharded into N slabs with RCCL halo exchange (strong scaling: the same
 problem on more GPUs); value = outer iterations of that one problem per second.
+
+At N = 1 the line also carries a "gn" object: the GN baseline (classical.py)
+solved on the GPU at 640x480 and 320x240, and the oracle's SuperLU solve of the 320x240 pair on
+one host core beside it.
 
 Prints ONE JSON line on rank 0.
 """
@@ -39,7 +43,9 @@ def parse():
     ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "2")),
                     help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gn", action="store_true", help="skip the GN (classical.py, config 3) side measurement")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--gn-cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch HIP-event pass (roofline fields become null)")
     return ap.parse_args()
@@ -79,10 +85,58 @@ def cpu_baseline_child():
     print(json.dumps({"loop_s": loop, "assemble_s": total, "cg_its": int(its)}))
 
 
+GN_W, GN_H, GN_ALPHA, GN_LAMBDA = 640, 480, 0.1, 0.2   # config 3 size, run.sh:103 parameters
+GN_CPU_W, GN_CPU_H = 320, 240                          # bounded CPU sample (spsolve ~13 s here)
+
+
+def gn_cpu_child():
+    """The oracle's GN solve (classical.py:113-130: SuperLU spsolve) on the CPU sample pair."""
+    sys.path.insert(0, REPO)
+    from oracle import foto_oracle as O
+    from foto.synthetic import sinusoid_pair
+    f1, f2 = sinusoid_pair(GN_CPU_W, GN_CPU_H)
+    t = time.perf_counter()
+    O.gn_solve(f1, f2, GN_CPU_W, GN_CPU_H, GN_ALPHA, GN_LAMBDA)
+    print(json.dumps({"solve_s": time.perf_counter() - t}))
+
+
+def gn_side(with_cpu):
+    """GN baseline (SURVEY.md §8(d) config 3 stand-in: sinusoid pair, alpha 0.1, lambda 0.2):
+    GPU PCG solve time at 640x480 and at the CPU sample size, the oracle's spsolve beside it."""
+    from foto import gn
+    from foto.synthetic import sinusoid_pair
+    out = {"workload": f"GN classical solve, sinusoid pair, alpha={GN_ALPHA}, lambda={GN_LAMBDA}, "
+                       f"block-Jacobi PCG to rtol {gn.GN_RTOL}"}
+    for (w, h) in ((GN_W, GN_H), (GN_CPU_W, GN_CPU_H)):
+        f1, f2 = sinusoid_pair(w, h)
+        best = None
+        for _ in range(2):
+            t = time.perf_counter()
+            _, _, _, info, its = gn.solve(f1, f2, w, h, GN_ALPHA, GN_LAMBDA)
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        out[f"gpu_{w}x{h}"] = {"solve_ms": round(1e3 * best, 2), "pcg_its": its, "info": info}
+    if with_cpu:
+        env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+        res = subprocess.run([sys.executable, os.path.abspath(__file__), "--gn-cpu-only"], env=env,
+                             capture_output=True, text=True, timeout=600)
+        if res.returncode == 0:
+            cpu_s = json.loads(res.stdout.strip().splitlines()[-1])["solve_s"]
+            gpu_s = out[f"gpu_{GN_CPU_W}x{GN_CPU_H}"]["solve_ms"] / 1e3
+            out["cpu_baseline"] = {"value_s": round(cpu_s, 3), "kind": "port", "cores": 1,
+                                   "sample": f"oracle spsolve (SuperLU, classical.py:113-130) on the "
+                                             f"{GN_CPU_W}x{GN_CPU_H} pair"}
+            out["speedup_vs_cpu"] = round(cpu_s / gpu_s, 1)
+    return out
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
         cpu_baseline_child()
+        return
+    if args.gn_cpu_only:
+        gn_cpu_child()
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,6 +255,8 @@ def main():
                                               f"({cb['cg_its']} CG its, {cb['loop_s']:.1f} s loop body)"}
             line["speedup_vs_cpu"] = round(value * cb["loop_s"], 1)
     s.close()
+    if line is not None and world == 1 and not args.no_gn:
+        line["gn"] = gn_side(with_cpu=not args.no_cpu_baseline)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

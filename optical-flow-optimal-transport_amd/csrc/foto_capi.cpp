@@ -287,23 +287,19 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
     Scope S;
     FOTO_TRY(S.init());
     const size_t n = (size_t)w * h;
-    double *d1, *d2, *fx, *fy, *ft, *b, *x, *r, *z, *p0, *p1, *part, *gath;
-    FOTO_TRY(S.up(f1, n, &d1));
-    FOTO_TRY(S.up(f2, n, &d2));
-    FOTO_TRY(S.dev(n, &fx));
-    FOTO_TRY(S.dev(n, &fy));
-    FOTO_TRY(S.dev(n, &ft));
-    FOTO_TRY(S.dev(3 * n, &b));
-    FOTO_TRY(S.dev(3 * n, &x));
-    FOTO_TRY(S.dev(3 * n, &r));
-    FOTO_TRY(S.dev(3 * n, &z));
-    FOTO_TRY(S.dev(3 * n, &p0));
-    FOTO_TRY(S.dev(3 * n, &p1));
+    double *d1, *d2, *fx, *fy, *ft, *b, *x, *r, *z, *p0, *p1, *part, *gath, *scal;
     const int nb = flat_blocks((int64_t)n);
-    FOTO_TRY(S.dev(2 * (size_t)nb + 8, &part));
-    FOTO_TRY(S.dev(8, &gath));
-    double* scal;
-    FOTO_TRY(S.dev(sizeof(CGScal) / sizeof(double) + 1, &scal));
+    {   // one allocation (a solve is ~15 ms; per-buffer hipMalloc/hipFree added up to ~1 ms)
+        const size_t nscal = sizeof(CGScal) / sizeof(double) + 1;
+        double* base;
+        FOTO_TRY(S.dev(23 * n + 2 * (size_t)nb + 8 + 8 + nscal, &base));
+        d1 = base; fx = base + 2 * n; fy = fx + n; ft = fy + n;
+        d2 = base + n;
+        b = ft + n; x = b + 3 * n; r = x + 3 * n; z = r + 3 * n; p0 = z + 3 * n; p1 = p0 + 3 * n;
+        part = p1 + 3 * n; gath = part + 2 * (size_t)nb + 8; scal = gath + 8;
+        FOTO_HIP_CHECK(hipMemcpyAsync(d1, f1, n * sizeof(double), hipMemcpyHostToDevice, S.s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(d2, f2, n * sizeof(double), hipMemcpyHostToDevice, S.s));
+    }
     CGScal* dS = (CGScal*)scal;
     FOTO_HIP_CHECK(hipMemsetAsync(part + 2 * nb, 0, 8 * sizeof(double), S.s));
     FOTO_HIP_CHECK(hipMemsetAsync(dS, 0, sizeof(CGScal), S.s));
@@ -319,17 +315,69 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
     std::unique_ptr<CGScal, void (*)(CGScal*)> hguard(hS, [](CGScal* p) { (void)hipHostFree(p); });
     int k = 0;
     bool done = false;
-    while (k < maxiter) {
-        const int chunk = std::min(k == 0 ? 64 : 32, maxiter - k);
-        for (int j = 0; j < chunk; ++j, ++k) {
-            double* po = (k & 1) ? p1 : p0;
-            double* pn = (k & 1) ? p0 : p1;
-            FOTO_HIP_CHECK(launch_gn_pcg_dir(w, h, k, fx, fy, d2, alpha, lam, z, po, pn, dS, rb, g_rz, g_pq, rtol, S.s));
-            FOTO_HIP_CHECK(launch_gn_pcg_upd(w, h, k, fx, fy, d2, alpha, lam, pn, x, r, z, dS, rb, g_pq, g_rz, S.s));
+    const char* emg = getenv("FOTO_GN_MG");   // 0: 3x3 block-Jacobi preconditioner (A/B runs)
+    if (!(emg && atoi(emg) == 0)) {
+        // Multigrid-preconditioned CG (foto_gn.hip): the init above already formed z with the
+        // block-Jacobi preconditioner; redo r = b, r.r and z = V(r), r.z.  Two iterations
+        // (p0 -> p1 -> p0) are captured once as a hipGraph (about 2 x (3 + 4 levels) small
+        // launches; the kernels read the iteration index from the device) and replayed.
+        GnMG mg;
+        FOTO_TRY(mg.setup(w, h, fx, fy, d2, alpha, lam, S.s));
+        FOTO_HIP_CHECK(launch_gn_mg_init((int64_t)n, b, r, rb, g_rz, S.s));
+        FOTO_TRY(mg.vcycle(r, z, dS, rb, g_rz, S.s));
+        auto iteration = [&](double* po, double* pn) -> int {
+            FOTO_HIP_CHECK(launch_gn_pcg_dir(w, h, -1, fx, fy, d2, alpha, lam, z, po, pn, dS, rb, g_rz, g_pq, rtol, S.s));
+            FOTO_HIP_CHECK(launch_gn_mg_upd(w, h, fx, fy, d2, alpha, lam, pn, x, r, dS, rb, g_pq, g_rz, S.s));
+            return mg.vcycle(r, z, dS, rb, g_rz, S.s);
+        };
+        const char* eg = getenv("FOTO_GN_GRAPH");
+        if (eg && atoi(eg) == 0) {   // direct launches (A/B runs)
+            while (k < maxiter) {
+                const int chunk = std::min(k == 0 ? 16 : 8, maxiter - k);
+                for (int j = 0; j < chunk; ++j, ++k) FOTO_TRY((k & 1) ? iteration(p1, p0) : iteration(p0, p1));
+                FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
+                FOTO_TRY(S.sync());
+                if (hS->done) { done = true; break; }
+            }
+            k = maxiter;   // skip the graph loop below
         }
-        FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
-        FOTO_TRY(S.sync());
-        if (hS->done) { done = true; break; }
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t gexec = nullptr;
+        FOTO_HIP_CHECK(hipStreamBeginCapture(S.s, hipStreamCaptureModeThreadLocal));
+        const int c1 = iteration(p0, p1), c2 = c1 < 0 ? c1 : iteration(p1, p0);
+        const hipError_t ec = hipStreamEndCapture(S.s, &graph);
+        std::unique_ptr<void, void (*)(void*)> gg(graph, [](void* g) { if (g) (void)hipGraphDestroy((hipGraph_t)g); });
+        FOTO_TRY(c2);
+        FOTO_HIP_CHECK(ec);
+        FOTO_HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+        std::unique_ptr<void, void (*)(void*)> ge(gexec, [](void* g) { (void)hipGraphExecDestroy((hipGraphExec_t)g); });
+        while (k < maxiter) {
+            const int chunk = std::min(k == 0 ? 16 : 8, maxiter - k);
+            int j = 0;
+            for (; j + 2 <= chunk; j += 2, k += 2) FOTO_HIP_CHECK(hipGraphLaunch(gexec, S.s));
+            if (j < chunk) {   // odd maxiter: one last iteration outside the graph (k even: p0 -> p1)
+                FOTO_TRY(iteration(p0, p1));
+                ++k;
+            }
+            FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
+            FOTO_TRY(S.sync());
+            if (hS->done) { done = true; break; }
+        }
+    } else {
+        while (k < maxiter) {
+            const int chunk = std::min(k == 0 ? 64 : 32, maxiter - k);
+            for (int j = 0; j < chunk; ++j, ++k) {
+                double* po = (k & 1) ? p1 : p0;
+                double* pn = (k & 1) ? p0 : p1;
+                FOTO_HIP_CHECK(launch_gn_pcg_dir(w, h, k, fx, fy, d2, alpha, lam, z, po, pn, dS, rb, g_rz, g_pq, rtol,
+                                                 S.s));
+                FOTO_HIP_CHECK(launch_gn_pcg_upd(w, h, k, fx, fy, d2, alpha, lam, pn, x, r, z, dS, rb, g_pq, g_rz,
+                                                 S.s));
+            }
+            FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
+            FOTO_TRY(S.sync());
+            if (hS->done) { done = true; break; }
+        }
     }
     FOTO_TRY(S.down(u, x, n));
     FOTO_TRY(S.down(v, x + n, n));

@@ -258,13 +258,14 @@ hipError_t launch_gn_pcg_init(int w, int h, const double* fx, const double* fy, 
 // Iteration k, first half: stop test on ||r||, beta = rz / rz_prev, p = z + beta p (computed
 // for the pixel and its 4 neighbours), q = A p, partial p.q; writes p.
 // gath_rz = {r.r, r.z} of r_k; gath_pq = {p.q}.
-__global__ __launch_bounds__(NT) void k_gn_pcg_dir(int w, int h, int k, const double* __restrict__ fx,
+__global__ __launch_bounds__(NT) void k_gn_pcg_dir(int w, int h, int k_arg, const double* __restrict__ fx,
                                                    const double* __restrict__ fy, const double* __restrict__ f2,
                                                    double a, double l, const double* __restrict__ z,
                                                    const double* __restrict__ po, double* __restrict__ pn, CGScal* S,
                                                    RedBuf rb, const double* __restrict__ gath_rz,
                                                    double* __restrict__ gath_pq, double rtol) {
     if (S->done) return;
+    const int k = k_arg >= 0 ? k_arg : S->pad[0];   // k < 0: iteration index kept on the device (MG path)
     const double rr = gath_rz[0], rz = gath_rz[1];
     const double atol = (k == 0) ? fmax(0.0, rtol * sqrt(rr)) : S->atol;
     if (rr == 0.0 || sqrt(rr) < atol) {
@@ -346,6 +347,468 @@ hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double
                              const double* gath_pq, double* gath_rz, hipStream_t s) {
     k_gn_pcg_upd<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, k, fx, fy, f2, alpha, lam, p, x, r, z, S, rb,
                                                             gath_pq, gath_rz);
+    return hipGetLastError();
+}
+
+
+// ============================================================================ multigrid preconditioner
+//
+// PCG on the GN system (classical.py:68-130) preconditioned by one symmetric V-cycle:
+// cell-centred levels (w, h) -> (ceil(w/2), ceil(h/2)) down to at most MG_COARSE cells;
+// operator on level l: s_f (-Lambda) x_f + B x per cell, s = (alpha, alpha, lambda) / 4^l (the
+// h^2 scaling of a 5-point Neumann Laplacian rediscretised on a grid twice as coarse),
+// B = the pointwise 3x3 coupling v v^T (v = (fx, fy, -f2)) on level 0 and the average of the
+// children's B (weighted like R B P) below; prolongation P = cell-centred bilinear (weights
+// 3/4, 1/4 per axis, indices clamped at the Neumann boundary), restriction R = P^T / 4;
+// one damped (omega = 0.8) block-Jacobi sweep before and after the coarse correction, the
+// coarsest level smoothed MG_CSWEEPS times from zero in one block.  Every piece is a fixed
+// symmetric linear operator, so the V-cycle is a valid CG preconditioner.  Numpy prototype
+// (320x240 sinusoid pair, rtol 1e-10): 33 PCG iterations instead of ~940 with the 3x3
+// block-Jacobi preconditioner; the solve still meets SuperLU's answer to ~1e-9.
+// Any approximation here only changes the preconditioner: the PCG applies the exact operator
+// (gn_row, CSR order) and stops on the exact residual norm.
+
+constexpr int MG_COARSE = 1024;   // cells of the coarsest level (one block, one cell per thread)
+constexpr int MG_CSWEEPS = 48;
+constexpr double MG_OMEGA = 0.8;
+
+struct MGLev {
+    int w, h;
+    double s0, s1, s2;
+    const double* B;      // 6 planes: bxx bxy bxm byy bym bmm
+    const double* Dinv;   // 6 planes: inverse of the cell's 3x3 diagonal block (symmetric)
+};
+
+__device__ __forceinline__ int mg_ncount(int x, int y, int w, int h) {
+    return (x > 0) + (x < w - 1) + (y > 0) + (y < h - 1);
+}
+
+// 1-D weight of coarse index I for fine index i (n fine cells, nc coarse), clamped
+__device__ __forceinline__ double mg_w1(int i, int I, int nc) {
+    const int I0 = i >> 1;
+    int I1 = (i & 1) ? I0 + 1 : I0 - 1;
+    I1 = I1 < 0 ? 0 : (I1 > nc - 1 ? nc - 1 : I1);
+    return (I0 == I ? 0.75 : 0.0) + (I1 == I ? 0.25 : 0.0);
+}
+
+// (A x)_f for cell (x, y) of level L; X(f, idx) loads the vector
+template <class F>
+__device__ __forceinline__ void mg_apply(const MGLev& L, int x, int y, int64_t i, F X, double& a0, double& a1,
+                                         double& a2) {
+    const int64_t n = (int64_t)L.w * L.h;
+    const int64_t jxm = x > 0 ? i - 1 : i, jxp = x < L.w - 1 ? i + 1 : i;
+    const int64_t jym = y > 0 ? i - L.w : i, jyp = y < L.h - 1 ? i + L.w : i;
+    const double c = (double)mg_ncount(x, y, L.w, L.h);
+    double v[3], nb[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        v[f] = X(f, i);
+        const double xm = X(f, jxm), xp = X(f, jxp), ym = X(f, jym), yp = X(f, jyp);
+        nb[f] = (x > 0 ? xm : 0.0) + (x < L.w - 1 ? xp : 0.0) + (y > 0 ? ym : 0.0) + (y < L.h - 1 ? yp : 0.0);
+    }
+    const double* B = L.B;
+    const double bxx = B[i], bxy = B[n + i], bxm = B[2 * n + i], byy = B[3 * n + i], bym = B[4 * n + i],
+                 bmm = B[5 * n + i];
+    a0 = L.s0 * (c * v[0] - nb[0]) + bxx * v[0] + bxy * v[1] + bxm * v[2];
+    a1 = L.s1 * (c * v[1] - nb[1]) + bxy * v[0] + byy * v[1] + bym * v[2];
+    a2 = L.s2 * (c * v[2] - nb[2]) + bxm * v[0] + bym * v[1] + bmm * v[2];
+}
+
+__device__ __forceinline__ void mg_dinv(const MGLev& L, int64_t i, double r0, double r1, double r2, double& z0,
+                                        double& z1, double& z2) {
+    const int64_t n = (int64_t)L.w * L.h;
+    const double* D = L.Dinv;
+    const double d00 = D[i], d01 = D[n + i], d02 = D[2 * n + i], d11 = D[3 * n + i], d12 = D[4 * n + i],
+                 d22 = D[5 * n + i];
+    z0 = d00 * r0 + d01 * r1 + d02 * r2;
+    z1 = d01 * r0 + d11 * r1 + d12 * r2;
+    z2 = d02 * r0 + d12 * r1 + d22 * r2;
+}
+
+__global__ __launch_bounds__(NT) void k_mg_b0(int64_t n, const double* __restrict__ fx, const double* __restrict__ fy,
+                                              const double* __restrict__ f2, double* __restrict__ B) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const double a = fx[i], b = fy[i], m = f2[i];
+    B[i] = a * a;
+    B[n + i] = a * b;
+    B[2 * n + i] = -a * m;
+    B[3 * n + i] = b * b;
+    B[4 * n + i] = -b * m;
+    B[5 * n + i] = m * m;
+}
+
+// coarse B = (sum of children B weighted by the P weights) / (sum of those weights)
+__global__ __launch_bounds__(NT) void k_mg_coarsen(int w, int h, const double* __restrict__ B, int wc, int hc,
+                                                   double* __restrict__ Bc) {
+    const int64_t nc = (int64_t)wc * hc, n = (int64_t)w * h;
+    const int64_t I = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (I >= nc) return;
+    const int J = (int)(I / wc), K = (int)(I - (int64_t)J * wc);
+    double acc[6] = {0, 0, 0, 0, 0, 0}, ws = 0.0;
+    for (int y = max(0, 2 * J - 2); y <= min(h - 1, 2 * J + 3); ++y) {
+        const double wy = mg_w1(y, J, hc);
+        if (wy == 0.0) continue;
+        for (int x = max(0, 2 * K - 2); x <= min(w - 1, 2 * K + 3); ++x) {
+            const double wgt = wy * mg_w1(x, K, wc);
+            if (wgt == 0.0) continue;
+            const int64_t i = (int64_t)y * w + x;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) acc[f] += wgt * B[f * n + i];
+            ws += wgt;
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < 6; ++f) Bc[f * nc + I] = acc[f] / ws;
+}
+
+// inverse of the 3x3 diagonal block diag(s c) + B (symmetric positive definite), cofactors
+__global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Dinv) {
+    const int64_t n = (int64_t)L.w * L.h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int y = (int)(i / L.w), x = (int)(i - (int64_t)y * L.w);
+    const double c = (double)mg_ncount(x, y, L.w, L.h);
+    const double* B = L.B;
+    const double a = L.s0 * c + B[i], b = B[n + i], d = B[2 * n + i], e = L.s1 * c + B[3 * n + i],
+                 f = B[4 * n + i], g = L.s2 * c + B[5 * n + i];
+    // [[a b d] [b e f] [d f g]]
+    const double c00 = e * g - f * f, c01 = d * f - b * g, c02 = b * f - d * e;
+    const double c11 = a * g - d * d, c12 = b * d - a * f, c22 = a * e - b * b;
+    const double det = a * c00 + b * c01 + d * c02, id = 1.0 / det;
+    Dinv[i] = c00 * id;
+    Dinv[n + i] = c01 * id;
+    Dinv[2 * n + i] = c02 * id;
+    Dinv[3 * n + i] = c11 * id;
+    Dinv[4 * n + i] = c12 * id;
+    Dinv[5 * n + i] = c22 * id;
+}
+
+// pre-smoothing from zero fused with the residual: x = omega D^-1 f, r = f - A x
+__global__ __launch_bounds__(NT) void k_mg_down(MGLev L, const CGScal* S, const double* __restrict__ f,
+                                                double* __restrict__ x, double* __restrict__ r) {
+    if (S->done) return;
+    const int64_t n = (int64_t)L.w * L.h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int y = (int)((unsigned)i / (unsigned)L.w), xx = (int)i - y * L.w;
+    auto X = [&](int fld, int64_t j) {
+        double z0, z1, z2;
+        mg_dinv(L, j, f[j], f[n + j], f[2 * n + j], z0, z1, z2);
+        return MG_OMEGA * (fld == 0 ? z0 : (fld == 1 ? z1 : z2));
+    };
+    double a0, a1, a2;
+    mg_apply(L, xx, y, i, X, a0, a1, a2);
+    x[i] = X(0, i);
+    x[n + i] = X(1, i);
+    x[2 * n + i] = X(2, i);
+    r[i] = f[i] - a0;
+    r[n + i] = f[n + i] - a1;
+    r[2 * n + i] = f[2 * n + i] - a2;
+}
+
+// fc = R r = P^T r / 4
+__global__ __launch_bounds__(NT) void k_mg_restrict(int w, int h, const CGScal* S, const double* __restrict__ r,
+                                                    int wc, int hc, double* __restrict__ fc) {
+    if (S->done) return;
+    const int64_t nc = (int64_t)wc * hc, n = (int64_t)w * h;
+    const int64_t I = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (I >= nc) return;
+    const int J = (int)(I / wc), K = (int)(I - (int64_t)J * wc);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    for (int y = max(0, 2 * J - 2); y <= min(h - 1, 2 * J + 3); ++y) {
+        const double wy = mg_w1(y, J, hc);
+        if (wy == 0.0) continue;
+        for (int x = max(0, 2 * K - 2); x <= min(w - 1, 2 * K + 3); ++x) {
+            const double wgt = wy * mg_w1(x, K, wc);
+            if (wgt == 0.0) continue;
+            const int64_t i = (int64_t)y * w + x;
+            a0 += wgt * r[i];
+            a1 += wgt * r[n + i];
+            a2 += wgt * r[2 * n + i];
+        }
+    }
+    fc[I] = 0.25 * a0;
+    fc[nc + I] = 0.25 * a1;
+    fc[2 * nc + I] = 0.25 * a2;
+}
+
+// x += P ec
+__global__ __launch_bounds__(NT) void k_mg_prolong(int w, int h, const CGScal* S, const double* __restrict__ ec,
+                                                   int wc, int hc, double* __restrict__ x) {
+    if (S->done) return;
+    const int64_t n = (int64_t)w * h, nc = (int64_t)wc * hc;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int y = (int)((unsigned)i / (unsigned)w), xx = (int)i - y * w;
+    const int X0 = xx >> 1, Y0 = y >> 1;
+    int X1 = (xx & 1) ? X0 + 1 : X0 - 1, Y1 = (y & 1) ? Y0 + 1 : Y0 - 1;
+    X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
+    Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
+    const int64_t c00 = (int64_t)Y0 * wc + X0, c01 = (int64_t)Y0 * wc + X1, c10 = (int64_t)Y1 * wc + X0,
+                  c11 = (int64_t)Y1 * wc + X1;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        const double* e = ec + f * nc;
+        x[f * n + i] += 0.5625 * e[c00] + 0.1875 * e[c01] + 0.1875 * e[c10] + 0.0625 * e[c11];
+    }
+}
+
+// xo = xi + omega D^-1 (f - A xi); RZ: partial sum of f . xo -> gath_rz[1] (the PCG's r.z)
+template <bool RZ>
+__global__ __launch_bounds__(NT) void k_mg_smooth(MGLev L, const CGScal* S, const double* __restrict__ f,
+                                                  const double* __restrict__ xi, double* __restrict__ xo,
+                                                  RedBuf rb, double* gath_rz) {
+    if (S->done) return;
+    const int64_t n = (int64_t)L.w * L.h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double rz = 0.0;
+    if (i < n) {
+        const int y = (int)((unsigned)i / (unsigned)L.w), xx = (int)i - y * L.w;
+        double a0, a1, a2, z0, z1, z2;
+        mg_apply(L, xx, y, i, [&](int fld, int64_t j) { return xi[fld * n + j]; }, a0, a1, a2);
+        const double f0 = f[i], f1 = f[n + i], f2v = f[2 * n + i];
+        mg_dinv(L, i, f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
+        const double o0 = xi[i] + MG_OMEGA * z0, o1 = xi[n + i] + MG_OMEGA * z1, o2 = xi[2 * n + i] + MG_OMEGA * z2;
+        xo[i] = o0;
+        xo[n + i] = o1;
+        xo[2 * n + i] = o2;
+        rz = f0 * o0 + f1 * o1 + f2v * o2;
+    }
+    if constexpr (RZ) {
+        double v[1] = {rz}, tot[1];
+        if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rz[1] = tot[0];
+    }
+}
+
+// coarsest level: MG_CSWEEPS damped block-Jacobi sweeps from zero in one block (x in LDS, each
+// thread's cell coefficients in registers: a sweep touches no global memory);
+// RZ (single-level hierarchy): also f . x -> gath_rz[1]
+template <bool RZ>
+__global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, const double* __restrict__ f,
+                                                     double* __restrict__ xout, double* gath_rz) {
+    if (S->done) return;
+    __shared__ double xs[2][3 * MG_COARSE];
+    __shared__ double red[16];
+    const int n = L.w * L.h, i = threadIdx.x;
+    const bool in = i < n;
+    const int y = in ? i / L.w : 0, xx = in ? i - y * L.w : 0;
+    double f0 = 0, f1 = 0, f2v = 0;
+    double b[6] = {0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
+    const bool hxm = xx > 0, hxp = xx < L.w - 1, hym = y > 0, hyp = y < L.h - 1;
+    const double c = (double)mg_ncount(xx, y, L.w, L.h);
+    if (in) {
+        f0 = f[i]; f1 = f[n + i]; f2v = f[2 * n + i];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { b[k] = L.B[k * n + i]; d[k] = L.Dinv[k * n + i]; }
+        const double z0 = d[0] * f0 + d[1] * f1 + d[2] * f2v, z1 = d[1] * f0 + d[3] * f1 + d[4] * f2v,
+                     z2 = d[2] * f0 + d[4] * f1 + d[5] * f2v;
+        xs[0][i] = MG_OMEGA * z0; xs[0][n + i] = MG_OMEGA * z1; xs[0][2 * n + i] = MG_OMEGA * z2;
+    }
+    __syncthreads();
+    const double sc[3] = {L.s0, L.s1, L.s2};
+    int cur = 0;
+    for (int sweep = 1; sweep < MG_CSWEEPS; ++sweep) {
+        if (in) {
+            const double* xc = xs[cur];
+            double v[3], a[3];
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) {
+                const double* q = xc + fl * n;
+                v[fl] = q[i];
+                const double nb = (hxm ? q[i - 1] : 0.0) + (hxp ? q[i + 1] : 0.0) + (hym ? q[i - L.w] : 0.0) +
+                                  (hyp ? q[i + L.w] : 0.0);
+                a[fl] = sc[fl] * (c * v[fl] - nb);
+            }
+            const double r0 = f0 - (a[0] + b[0] * v[0] + b[1] * v[1] + b[2] * v[2]);
+            const double r1 = f1 - (a[1] + b[1] * v[0] + b[3] * v[1] + b[4] * v[2]);
+            const double r2 = f2v - (a[2] + b[2] * v[0] + b[4] * v[1] + b[5] * v[2]);
+            xs[cur ^ 1][i] = v[0] + MG_OMEGA * (d[0] * r0 + d[1] * r1 + d[2] * r2);
+            xs[cur ^ 1][n + i] = v[1] + MG_OMEGA * (d[1] * r0 + d[3] * r1 + d[4] * r2);
+            xs[cur ^ 1][2 * n + i] = v[2] + MG_OMEGA * (d[2] * r0 + d[4] * r1 + d[5] * r2);
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+    double rz = 0.0;
+    if (in) {
+        xout[i] = xs[cur][i]; xout[n + i] = xs[cur][n + i]; xout[2 * n + i] = xs[cur][2 * n + i];
+        rz = f0 * xs[cur][i] + f1 * xs[cur][n + i] + f2v * xs[cur][2 * n + i];
+    }
+    if constexpr (RZ) {
+        rz = gn_wave_sum(rz);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = rz;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int w = 0; w < 16; ++w) s += red[w];
+            gath_rz[1] = s;
+        }
+    }
+}
+
+// PCG pieces without the block-Jacobi preconditioner (the V-cycle supplies z):
+// init: r = b, r.r -> gath_rz[0]; upd: x += alpha p, r -= alpha A p, r.r -> gath_rz[0]
+__global__ __launch_bounds__(NT) void k_gn_mg_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
+                                                   RedBuf rb, double* gath_rz) {
+    double rr = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < 3 * n; i += (int64_t)gridDim.x * NT) {
+        const double v = b[i];
+        r[i] = v;
+        rr += v * v;
+    }
+    double v[1] = {rr}, tot[1];
+    if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rz[0] = tot[0];
+}
+
+__global__ __launch_bounds__(NT) void k_gn_mg_upd(int w, int h, const double* __restrict__ fx,
+                                                  const double* __restrict__ fy, const double* __restrict__ f2,
+                                                  double a, double l, const double* __restrict__ p,
+                                                  double* __restrict__ x, double* __restrict__ r, CGScal* S,
+                                                  RedBuf rb, const double* __restrict__ gath_pq,
+                                                  double* __restrict__ gath_rz) {
+    if (S->done) return;
+    const int k = S->pad[0];
+    const double alpha = S->rho / gath_pq[0];
+    const int64_t n = (int64_t)w * h;
+    double rr = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        const GNPix P = gn_pix(w, h, i);
+        double qu, qv, qm;
+        gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, [&](int f, int64_t j) { return p[f * n + j]; }, qu, qv, qm);
+        const double q3[3] = {qu, qv, qm};
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const int64_t o = f * n + i;
+            const double ap = alpha * p[o];
+            x[o] = (k == 0) ? 0.0 + ap : x[o] + ap;
+            const double rn = r[o] - alpha * q3[f];
+            r[o] = rn;
+            rr += rn * rn;
+        }
+    }
+    double v[1] = {rr}, tot[1];
+    if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) {
+        gath_rz[0] = tot[0];
+        S->pad[0] = k + 1;   // iteration index kept on the device (graph replays carry none)
+    }
+}
+
+// ---------------------------------------------------------------------------- host side
+
+int GnMG::setup(int w, int h, const double* fx, const double* fy, const double* f2, double alpha, double lam,
+                hipStream_t s) {
+    free_all();
+    int lw = w, lh = h;
+    double sc = 1.0;
+    size_t total = 0;
+    for (;;) {   // level geometry first, then one allocation for the whole hierarchy
+        Lev L;
+        L.w = lw;
+        L.h = lh;
+        L.s[0] = alpha * sc; L.s[1] = alpha * sc; L.s[2] = lam * sc;
+        total += 24 * (size_t)lw * lh;
+        lev.push_back(L);
+        if ((int64_t)lw * lh <= MG_COARSE) break;
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+        sc *= 0.25;
+    }
+    double* base = nullptr;
+    FOTO_TRY(alloc(total, &base));
+    for (Lev& L : lev) {
+        const size_t n = (size_t)L.w * L.h;
+        L.B = base; base += 6 * n;
+        L.Dinv = base; base += 6 * n;
+        L.f = base; base += 3 * n;
+        L.x = base; base += 3 * n;
+        L.y = base; base += 3 * n;
+        L.r = base; base += 3 * n;
+    }
+    const int64_t n0 = (int64_t)w * h;
+    k_mg_b0<<<flat_blocks(n0), NT, 0, s>>>(n0, fx, fy, f2, lev[0].B);
+    FOTO_HIP_CHECK(hipGetLastError());
+    for (size_t l = 1; l < lev.size(); ++l) {
+        const int64_t nc = (int64_t)lev[l].w * lev[l].h;
+        k_mg_coarsen<<<flat_blocks(nc), NT, 0, s>>>(lev[l - 1].w, lev[l - 1].h, lev[l - 1].B, lev[l].w, lev[l].h,
+                                                   lev[l].B);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    for (size_t l = 0; l < lev.size(); ++l) {
+        const int64_t n = (int64_t)lev[l].w * lev[l].h;
+        k_mg_dinv<<<flat_blocks(n), NT, 0, s>>>(desc(l), lev[l].Dinv);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
+MGLev GnMG::desc(size_t l) const {
+    const Lev& L = lev[l];
+    return MGLev{L.w, L.h, L.s[0], L.s[1], L.s[2], L.B, L.Dinv};
+}
+
+// z = V(r); r.z -> gath_rz[1]
+int GnMG::vcycle(const double* r, double* z, const CGScal* S, RedBuf rb, double* gath_rz, hipStream_t s) {
+    const size_t nl = lev.size();
+    if (nl == 1) {
+        k_mg_coarse<true><<<1, 1024, 0, s>>>(desc(0), S, r, z, gath_rz);
+        FOTO_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    // down
+    for (size_t l = 0; l + 1 < nl; ++l) {
+        const Lev& L = lev[l];
+        const int64_t n = (int64_t)L.w * L.h, nc = (int64_t)lev[l + 1].w * lev[l + 1].h;
+        const double* f = (l == 0) ? r : L.f;
+        k_mg_down<<<flat_blocks(n), NT, 0, s>>>(desc(l), S, f, L.x, L.r);
+        FOTO_HIP_CHECK(hipGetLastError());
+        k_mg_restrict<<<flat_blocks(nc), NT, 0, s>>>(L.w, L.h, S, L.r, lev[l + 1].w, lev[l + 1].h, lev[l + 1].f);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    const size_t c = nl - 1;
+    k_mg_coarse<false><<<1, 1024, 0, s>>>(desc(c), S, lev[c].f, lev[c].x, nullptr);
+    FOTO_HIP_CHECK(hipGetLastError());
+    // up: the coarser level's correction sits in its x (coarsest) or y (post-smoothed)
+    const double* e = lev[c].x;
+    for (size_t l = nl - 1; l-- > 0;) {
+        const Lev& L = lev[l];
+        const int64_t n = (int64_t)L.w * L.h;
+        k_mg_prolong<<<flat_blocks(n), NT, 0, s>>>(L.w, L.h, S, e, lev[l + 1].w, lev[l + 1].h, L.x);
+        FOTO_HIP_CHECK(hipGetLastError());
+        if (l == 0) {
+            k_mg_smooth<true><<<flat_blocks(n), NT, 0, s>>>(desc(0), S, r, L.x, z, rb, gath_rz);
+        } else {
+            k_mg_smooth<false><<<flat_blocks(n), NT, 0, s>>>(desc(l), S, L.f, L.x, L.y, rb, nullptr);
+            e = L.y;
+        }
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
+int GnMG::alloc(size_t n_doubles, double** p) {
+    FOTO_HIP_CHECK(hipMalloc((void**)p, std::max<size_t>(n_doubles, 1) * sizeof(double)));
+    bufs.push_back(*p);
+    return 0;
+}
+
+void GnMG::free_all() {
+    for (void* p : bufs) (void)hipFree(p);
+    bufs.clear();
+    lev.clear();
+}
+
+hipError_t launch_gn_mg_init(int64_t n, const double* b, double* r, RedBuf rb, double* gath_rz, hipStream_t s) {
+    // grid sized by n (not 3 n): the reduction scratch holds 2 partials per block of n
+    k_gn_mg_init<<<gn_grid(n), NT, 0, s>>>(n, b, r, rb, gath_rz);
+    return hipGetLastError();
+}
+
+hipError_t launch_gn_mg_upd(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
+                            double lam, const double* p, double* x, double* r, CGScal* S, RedBuf rb,
+                            const double* gath_pq, double* gath_rz, hipStream_t s) {
+    k_gn_mg_upd<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, fx, fy, f2, alpha, lam, p, x, r, S, rb, gath_pq,
+                                                         gath_rz);
     return hipGetLastError();
 }
 
