@@ -567,7 +567,7 @@ int foto_bb_opts_default(foto_bb_opts* o) {
     o->device = -1;
     o->cg_maxiter = 1000;
     o->cg_rtol = 1e-6;
-    o->cg_mode = 0;
+    o->cg_mode = 2;   // spectral s-step CG (falls back to the stencil CG when eps <= 0)
     o->rank = 0;
     o->world = 1;
     o->nccl_id = nullptr;
@@ -606,6 +606,9 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
     if (o.world > 1 && o.virtual_ranks > 1) { set_error("virtual_ranks requires world == 1"); return FOTO_ERR_ARG; }
     if (o.world > 1 && !o.nccl_id) { set_error("world > 1 needs nccl_id"); return FOTO_ERR_ARG; }
     if (o.cg_maxiter < 0) { set_error("cg_maxiter < 0"); return FOTO_ERR_ARG; }
+    // the spectral CGs recover x = C^T((b^ - r^) / lam) and need lam > 0, i.e. eps > 0; with
+    // eps <= 0 (A singular, as the reference then runs it) only the stencil CG applies
+    if (o.cg_mode != 0 && !(reg_epsilon > 0.0)) o.cg_mode = 0;
     auto c = std::make_unique<foto_bb_ctx>();
     c->Nt = Nt; c->Nx = Nx; c->Ny = Ny; c->r = r; c->eps = reg_epsilon; c->o = o;
     c->rccl = o.world > 1;

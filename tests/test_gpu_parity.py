@@ -156,6 +156,32 @@ def test_bb_solve_small(gold, name, mode, capsys):
     assert out[-1].endswith(f"({len(d['crit'])}/{int(max_it)})")
 
 
+def test_bb_solve_c_entry_default(gold):
+    """foto_bb_solve, the one-shot C entry the INTEGRATION.md ctypes binding calls, at its
+    default CG (spectral s-step) matches the reference's golden solve; reg_epsilon = 0 falls
+    back to the stencil CG instead of failing (the spectral CGs divide by lam = r eps + ...)."""
+    import ctypes
+    from foto import _lib
+    d = gold("bb_small.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    crit = []
+    cb = _lib.ITER_CB(lambda user, i, c, its, info: crit.append(c))
+    u, v, m = (np.empty(Nx * Ny) for _ in range(3))
+    rho0 = np.ascontiguousarray(d["rho0"], dtype=np.float64)
+    rhoT = np.ascontiguousarray(d["rhoT"], dtype=np.float64)
+    rc = _lib.lib().foto_bb_solve(_lib.dptr(rho0), _lib.dptr(rhoT), Nt, Nx, Ny, float(r), float(tol), float(eps),
+                                  int(max_it), cb, None, _lib.dptr(u), _lib.dptr(v), _lib.dptr(m))
+    assert rc >= 0, _lib.lib().foto_last_error()
+    np.testing.assert_allclose(crit, d["crit"], rtol=1e-7, atol=0)
+    for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
+    rc = _lib.lib().foto_bb_solve(_lib.dptr(rho0), _lib.dptr(rhoT), Nt, Nx, Ny, float(r), float(tol), 0.0, 2,
+                                  _lib.ITER_CB(), None, _lib.dptr(u), _lib.dptr(v), _lib.dptr(m))
+    assert rc >= 0, _lib.lib().foto_last_error()
+    assert np.all(np.isfinite(u)) and np.all(np.isfinite(v))
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_bb_solve_c1(gold, mode):
     d = gold("bb_c1.npz")
