@@ -99,6 +99,8 @@ typedef struct {
     int64_t n_k[8];
     double ms_k[8];
     double bytes_k[8];        /* algorithmic HBM bytes per launch of that class         */
+    int cg_redo;              /* outer iterations whose deferred CG solve (see foto_bb.cpp) */
+                              /* outran its predicted passes and re-ran prox             */
 } foto_bb_stats;
 
 /* kernel classes reported in foto_bb_stats.n_k / ms_k / bytes_k */

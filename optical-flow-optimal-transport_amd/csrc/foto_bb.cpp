@@ -438,7 +438,22 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
     // phase boundaries are recorded, not waited on: the one host wait per outer iteration
     // is the crit readback below (a wait here idled the GPU for the host's wake-up)
     FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    FOTO_TRY(cg_solve(c, cg_iters, cg_info));
+    // Single shard, spectral s-step: once a solve has fixed the pass count, the solve is
+    // enqueued without a host wait and prox follows behind it, guarded by the CG's done flag;
+    // the one sync below (crit) then also delivers the CG result.  A solve that needs more
+    // passes than predicted (rare: the count changes by 0-1 between outer iterations) is
+    // finished after that sync, and prox re-runs (FOTO_CG_DEFER=0: always wait for the CG).
+    const char* de = getenv("FOTO_CG_DEFER");
+    const bool defer_on = !(de && atoi(de) == 0);
+    SpectralPlan* dsp = (defer_on && W == 1 && c->o.cg_mode != 0 && c->sh[0]->spec && c->sh[0]->spec->deferrable())
+                            ? c->sh[0]->spec.get()
+                            : nullptr;
+    if (dsp) {
+        Shard& s = *c->sh[0];
+        FOTO_TRY(dsp->solve_deferred(s.rv, s.phi, c->o.cg_rtol, c->o.cg_maxiter, &c->kt, c->s));
+    } else {
+        FOTO_TRY(cg_solve(c, cg_iters, cg_info));
+    }
     FOTO_HIP_CHECK(hipEventRecord(c->ph[2], c->s));
     c->have_phi = 1;
 
@@ -448,13 +463,31 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
         const double nv = (double)s.g.nloc * (double)s.g.nxy;
         hipEvent_t e = c->kt.start(c->s);
         FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
-                                   s.gath_crit(W), s.rank, c->s));
+                                   s.gath_crit(W), s.rank, c->s, dsp ? dsp->done_flag() : nullptr));
         c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
     }
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
     FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
     FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
     FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
+    if (dsp) {
+        int redo = 0;
+        FOTO_TRY(dsp->finish(cg_iters, cg_info, &redo, &c->kt, c->s));
+        c->last_cg = *cg_iters;
+        if (redo) {   // the guarded prox returned at once: drop its timing, run it on the final phi
+            Shard& s = *c->sh[0];
+            const double nv = (double)s.g.nloc * (double)s.g.nxy;
+            c->kt.discard_last(FOTO_K_PROX, 1);
+            hipEvent_t e = c->kt.start(c->s);
+            FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
+                                       s.gath_crit(W), s.rank, c->s));
+            c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+            FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
+            FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
+            c->st.cg_redo += 1;
+        }
+    }
     float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
     FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->ph[0], c->ph[1]));
     FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[1], c->ph[2]));

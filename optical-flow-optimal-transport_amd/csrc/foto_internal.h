@@ -169,7 +169,8 @@ hipError_t launch_cg_upd(const Geo& g, int k, const double* p, double* x, double
                          CGScal* S, RedBuf rb, const double* gath_pap, double* gath_rr, hipStream_t s);
 // grad_st phi -> stepB -> mu update -> crit partial sums (num, den) -> gath[2*rank..]
 hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
-                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s);
+                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s,
+                       const int* guard = nullptr);
 // trajectory steps n in [n_lo, n_hi) using phi planes (local plane index l = n - t0)
 hipError_t launch_traj(const Geo& g, const double* phi, int n_lo, int n_hi, double* px, double* py,
                        int init, hipStream_t s);

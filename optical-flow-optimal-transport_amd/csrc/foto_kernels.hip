@@ -555,9 +555,12 @@ __global__ __launch_bounds__(NT) void k_prox(Geo g, const double* __restrict__ p
                                              double* __restrict__ mux, double* __restrict__ muy,
                                              double* __restrict__ qt, double* __restrict__ qx,
                                              double* __restrict__ qy, double r, double inv_r, RedBuf rb,
-                                             double* gath, int rank) {
+                                             double* gath, int rank, const int* __restrict__ guard) {
     // 2.5-D march over phi (64 x 4 LDS tile + halo, t-neighbours in registers), then the
     // pointwise stepB / stepC / criterion terms of each voxel.
+    // guard: the CG's done flag when the host enqueued this without waiting for the solve; an
+    // unfinished solve leaves mu, q untouched and the host re-runs prox after finishing it.
+    if (guard && *guard == 0) return;
     const int64_t nxy = g.nxy;
     double num = 0.0, den = 0.0;
     march(g, blockIdx.x, [&](int l, int64_t off) { return phi[l * nxy + off]; },
@@ -590,8 +593,9 @@ __global__ __launch_bounds__(NT) void k_prox(Geo g, const double* __restrict__ p
 }
 
 hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
-                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s) {
-    k_prox<<<march_blocks(g), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, r, 1.0 / r, rb, gath, rank);
+                       double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s,
+                       const int* guard) {
+    k_prox<<<march_blocks(g), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, r, 1.0 / r, rb, gath, rank, guard);
     return hipGetLastError();
 }
 

@@ -11,6 +11,15 @@ struct SpectralPlan {
     // single shard: b (physical, clobbered) -> x (physical); scipy stopping rule.
     int solve(double* b, double* x, double rtol, int maxiter, int predicted, int* iters, int* info, KTimer* kt,
               hipStream_t s);
+    // Deferred variant (single shard, s-step, after a first solve has set the pass count):
+    // enqueues the predicted passes and the inverse transforms without waiting; the state
+    // travels to a pinned copy behind them.  done_flag() is the device flag a consumer can
+    // guard on.  After the caller's stream sync, finish() reports the result; if the passes
+    // did not suffice (*redo = 1) it runs the rest of the solve, polling, and recomputes x.
+    bool deferrable() const;
+    int solve_deferred(double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s);
+    const int* done_flag() const;
+    int finish(int* iters, int* info, int* redo, KTimer* kt, hipStream_t s);
 
     // ---- sharded phases (driven by foto_bb.cpp, all-to-all / all-gather in between)
     int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, pack -> stage

@@ -2081,6 +2081,11 @@ struct SpecImpl {
     bool tcol = false;            // single shard, s-step, Nt in FOTO_TCOL_SIZES
     int tcol_nb = 0;              // column kernels' blocks
     int last_passes = 0;          // passes of the previous s-step solve (first chunk size)
+    // deferred solve in flight (solve_deferred -> finish)
+    bool pending = false;
+    int pend_launched = 0, pend_maxiter = 0;
+    double pend_rtol = 0.0;
+    double *pend_b = nullptr, *pend_x = nullptr;
     int sstep = 1;
     bool split_plan = false;
     std::vector<void*> allocs;
@@ -2406,6 +2411,18 @@ static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* o
     return hipErrorNotSupported;
 }
 
+// (b^, r^) -t(+xhat)-> b -y-> tmp -x-> x
+static int tcol_inverse(SpecImpl* P, double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, b, rtol, maxiter, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, b, P->tmp, s));
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, P->tmp, x, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 7.0 * 8.0 * N);
+    return 0;
+}
+
 // single shard, s-step, column-kernel t axis: b -x-> tmp -y-> b -t(+INIT)-> b^; CG passes;
 // (b^, r^) -t(+xhat)-> b -y-> tmp -x-> x
 static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxiter, int predicted, int* iters,
@@ -2420,11 +2437,81 @@ static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxite
     FOTO_HIP_CHECK(launch_tcol(P, false, b, nullptr, rtol, maxiter, s));
     if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
     FOTO_TRY(solve_s2(P, rtol, maxiter, predicted, iters, info, kt, s, true));
-    e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, b, rtol, maxiter, s));
-    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, b, P->tmp, s));
-    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, P->tmp, x, s));
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 7.0 * 8.0 * N);
+    return tcol_inverse(P, b, x, rtol, maxiter, kt, s);
+}
+
+bool SpectralPlan::deferrable() const {
+    const SpecImpl* P = (const SpecImpl*)impl;
+    return P->tcol && P->sstep == 2 && P->world == 1 && P->last_passes > 0;
+}
+
+const int* SpectralPlan::done_flag() const { return &((const SpecImpl*)impl)->S2->done; }
+
+int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    if (!deferrable() || P->pending) {
+        set_error("spectral CG: deferred solve needs a single-shard s-step plan after a finished solve");
+        return FOTO_ERR_STATE;
+    }
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, b, s));
+    FOTO_HIP_CHECK(launch_tcol(P, false, b, nullptr, rtol, maxiter, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    // the previous solve's pass count + margin (passes past the end exit at once);
+    // FOTO_CG_MARGIN overrides the default 2 (tests force the redo path with a negative one)
+    const char* me = getenv("FOTO_CG_MARGIN");
+    const int margin = me ? atoi(me) : 2;
+    const int n = std::max(1, P->last_passes + margin);
+    for (int j = 0; j < n; ++j) {
+        hipEvent_t ep = kt ? kt->start(s) : nullptr;
+        FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, nullptr, s));
+        if (kt) kt->stop(ep, s, FOTO_K_SPEC, 32.0 * N);
+    }
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
+    FOTO_TRY(tcol_inverse(P, b, x, rtol, maxiter, kt, s));
+    P->pending = true;
+    P->pend_launched = n;
+    P->pend_b = b;
+    P->pend_x = x;
+    P->pend_rtol = rtol;
+    P->pend_maxiter = maxiter;
+    return 0;
+}
+
+int SpectralPlan::finish(int* iters, int* info, int* redo, KTimer* kt, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    if (!P->pending) {
+        set_error("spectral CG: no deferred solve to finish");
+        return FOTO_ERR_STATE;
+    }
+    P->pending = false;
+    *redo = 0;
+    int passes = P->pend_launched;
+    if (!P->hS2->done) {   // the predicted passes were not enough: continue, polling, and redo x
+        *redo = 1;
+        const double N = P->nbox();
+        while (!P->hS2->done) {
+            for (int j = 0; j < 2; ++j, ++passes) {
+                hipEvent_t e = kt ? kt->start(s) : nullptr;
+                FOTO_HIP_CHECK(launch_s2(P, false, P->pend_rtol, P->pend_maxiter, nullptr, s));
+                if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * N);
+            }
+            FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
+            FOTO_HIP_CHECK(hipStreamSynchronize(s));
+            if (passes > P->pend_maxiter + 4) {
+                set_error("spectral s-step CG did not terminate");
+                return FOTO_ERR_STATE;
+            }
+        }
+        FOTO_TRY(tcol_inverse(P, P->pend_b, P->pend_x, P->pend_rtol, P->pend_maxiter, kt, s));
+    }
+    *iters = P->hS2->iters;
+    *info = (P->hS2->done == 1) ? 0 : P->pend_maxiter;
+    P->last_passes = P->hS2->passes;
+    if (kt) kt->discard_last(FOTO_K_SPEC, std::max(0, passes - P->hS2->passes));
     return 0;
 }
 

@@ -52,6 +52,7 @@ class BBStats(ctypes.Structure):
         ("n_k", ctypes.c_int64 * 8),
         ("ms_k", ctypes.c_double * 8),
         ("bytes_k", ctypes.c_double * 8),
+        ("cg_redo", ctypes.c_int),
     ]
 
 

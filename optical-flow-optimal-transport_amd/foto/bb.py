@@ -139,7 +139,7 @@ class BBSolver:
         st = _lib.BBStats()
         check(lib().foto_bb_stats_get(self._ctx, ctypes.byref(st)))
         d = {f: getattr(st, f) for f in ("outer_iters", "cg_iters_total", "last_crit", "ms_rhs", "ms_cg",
-                                         "ms_prox", "ms_flow")}
+                                         "ms_prox", "ms_flow", "cg_redo")}
         d["kernels"] = {name: {"n": int(st.n_k[i]), "ms": float(st.ms_k[i]), "bytes": float(st.bytes_k[i])}
                         for i, name in enumerate(_lib.K_NAMES) if st.n_k[i] > 0}
         return d
