@@ -1609,8 +1609,9 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
                 if (i < ns) {   // guard, not break: keeps the loop fully unrolled (S0 out of scratch)
                     // iteration k + i: p = beta p + r (p = r at k = 0); r -= alpha (lam p)
                     const double a = S0.a[i], b = S0.b[i];
-                    const double p0 = (k + i == 0) ? r0 : fma(b, q0, r0);
-                    const double p1 = (k + i == 0) ? r1 : fma(b, q1, r1);
+                    // (k + i = 0: b = 0 and q = 0, so p = r)
+                    const double p0 = fma(b, q0, r0);
+                    const double p1 = fma(b, q1, r1);
                     r0 = fma(-a, e.l0 * p0, r0);
                     r1 = fma(-a, e.l1 * p1, r1);
                     q0 = p0;
@@ -1684,6 +1685,12 @@ __device__ __forceinline__ double lds_ld64(unsigned a) {
 }
 
 // wait until at most k vector-memory operations are outstanding (k wave-uniform; clamped)
+template <int N>
+__device__ __forceinline__ void vm_wait_imm() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ void vm_wait(int k) {
     switch (k) {
 #define FOTO_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
@@ -1783,7 +1790,14 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
     for (int j = 0; j < nj; ++j) {
         if (j + D - 1 < nj) ring_issue<D>(T, w, j + D - 1, src, ph, loadq);
         const int nG = min(j + D - 1, nj - 1) - j, nS = min(j, D - 1);
-        vm_wait(g * nG + NS * nS);
+        // steady state (D - 1 tiles ahead and behind) as one immediate wait; the switch over
+        // counts (a branch tree) only in the prologue and drain
+        if (nG == D - 1 && nS == D - 1) {
+            if (INIT || !loadq) vm_wait_imm<(1 + NS) * (D - 1)>();
+            else vm_wait_imm<(2 + NS) * (D - 1)>();
+        } else {
+            vm_wait(g * nG + NS * nS);
+        }
         const int u = w.gw + j * w.W;
         const int row = u / w.ntx, cx = u - row * w.ntx;
         const int kx = cx * 128 + 2 * lane;
@@ -1811,8 +1825,8 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
             for (int st = 0; st < SMAX; ++st) {
                 if (st < ns) {
                     const double a = S0.a[st], b = S0.b[st];
-                    const double p0 = (k + st == 0) ? r0 : fma(b, q0, r0);
-                    const double p1 = (k + st == 0) ? r1 : fma(b, q1, r1);
+                    const double p0 = fma(b, q0, r0);   // k + st = 0: b = 0, q = 0 (p = r)
+                    const double p1 = fma(b, q1, r1);
                     r0 = fma(-a, l0 * p0, r0);
                     r1 = fma(-a, l1 * p1, r1);
                     q0 = p0;
