@@ -1188,6 +1188,8 @@ struct SStep {
     int iters;    // iterations at finish
     int passes;   // plans made in this solve
     int flags;    // bit 0: no interval adaptation (A/B runs, FOTO_SADAPT=0)
+    int pend;     // the moments in gath await their plan (made at the start of the next pass)
+    int pad_;
     double a[SMAX], b[SMAX];
     double rho_prev;   // rho_{k-1}
     double atol;
@@ -1386,6 +1388,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         if (S.fin) {
             S.done = S.conv ? 1 : 2;
             S.nsteps = 0;
+            S.pend = 0;
             if (lane == 0) *Sg = S;
             return;
         }
@@ -1505,7 +1508,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
     if (lane == 0) {   // scalars only: a[], b[] were stored above
         Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
         Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
-        Sg->c0 = nc0; Sg->c1 = nc1; Sg->ic0 = ic0; Sg->ic1 = ic1;
+        Sg->c0 = nc0; Sg->c1 = nc1; Sg->ic0 = ic0; Sg->ic1 = ic1; Sg->pend = 0;
     }
 }
 
@@ -1712,8 +1715,9 @@ static inline bool ring_ok(const SpecTab& T) {
 }
 
 // Tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl).
-__device__ __forceinline__ void ring_stage_tables(const SpecTab& T, double* tab) {
-    for (int i = threadIdx.x; i < T.Nx + T.Nt + T.nyl; i += S2_NTH)
+// (first: the first thread taking part; a late-planning pass leaves wave 0 to its plan)
+__device__ __forceinline__ void ring_stage_tables(const SpecTab& T, double* tab, int first = 0) {
+    for (int i = (int)threadIdx.x - first; i >= 0 && i < T.Nx + T.Nt + T.nyl; i += S2_NTH - first)
         tab[i] = (i < T.Nx) ? T.mx[i] : (i < T.Nx + T.Nt) ? T.mt[i - T.Nx] : T.my[T.y0 + i - T.Nx - T.Nt];
 }
 
@@ -1849,29 +1853,109 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
     }
 }
 
+#ifdef FOTO_PLAN_CLOCK
+__device__ long long foto_plan_clock[4];
+#endif
+
+// SStep from LDS into wave-uniform registers (the plan made in LDS feeds the step loop's
+// scalar operands)
+__device__ __forceinline__ SStep sstep_uniform(const SStep* p) {
+    static_assert(sizeof(SStep) % 4 == 0, "SStep is whole dwords");
+    constexpr int NW = sizeof(SStep) / 4;
+    int wd[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) wd[i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(p)[i]);
+    SStep s;
+    __builtin_memcpy(&s, wd, sizeof s);
+    return s;
+}
+
+// FUSE (single shard): a working pass plans itself.  The pass that takes the moments leaves
+// them in gath with S.pend = 1; the next pass's blocks each make that plan at their start
+// (wave 0, identical inputs and code, so identical plans) while the other waves' first ring
+// tiles are already loading, instead of one block planning in the tail of the previous pass
+// with the whole chip idle behind it.  The last block (ticket) publishes the new moments and
+// state once every block has read the old ones.  A plan that finds the solve done still
+// passes the ticket, so that one block stores the final state.  INIT passes plan in their
+// tail (the fused t-DCT INIT and the ring INIT pass), leaving pend = 0.
 template <int D, bool INIT, bool FUSE>
 __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_spec_s2r(
         SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
         RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
+    constexpr bool LATE = FUSE && !INIT;
     __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
-    const SStep S0 = *Sg;
-    if (!INIT && (S0.done || S0.nsteps == 0)) return;
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
+    SStep S0 = *Sg;
+    if (!INIT && S0.done) return;
+    const bool late = LATE && S0.pend;
+    if (!INIT && !late && S0.nsteps == 0) return;
     double* tab = ring + RING_NW * D * RING_SLOT;
-    ring_stage_tables(T, tab);
-    __syncthreads();
+    __shared__ double tot[NACC];
+    const RingWave w = ring_wave(T, ring, D);
+    int issued = 0;
+    if constexpr (LATE) {
+        if (late) {
+            // Wave 0 plans at once: the previous pass's moments into LDS (its own lanes, so a
+            // wave-local wait orders them), its first tiles issued behind them, the plan.  The
+            // other waves stage the tables and issue their first tiles meanwhile.
+            __shared__ SStep Sl;
+            const int k = S0.k + S0.nsteps;
+            const double* src = (k == 0) ? bh : rh;
+            if (!S0.fin) issued = min(D - 1, w.nj);   // the plan will apply steps
+#ifdef FOTO_PLAN_CLOCK   // timing studies only (tools/pass_lab.hip): 100 MHz stamps of block 0
+            const long long c0 = wall_clock64();
+#endif
+            if (threadIdx.x < 64) {
+                if (threadIdx.x < NACC) tot[threadIdx.x] = gath[threadIdx.x];
+                if (threadIdx.x == 0) Sl = S0;
+                FOTO_LDS_WAIT();
+                for (int j = 0; j < issued; ++j) ring_issue<D>(T, w, j, src, ph, k > 0);
+                sstep_plan_wave(&Sl, S0, tot, xb, 0, rtol, maxiter);
+            } else {
+                ring_stage_tables(T, tab, 64);
+                for (int j = 0; j < issued; ++j) ring_issue<D>(T, w, j, src, ph, k > 0);
+            }
+#ifdef FOTO_PLAN_CLOCK
+            const long long c1 = wall_clock64();
+#endif
+            __syncthreads();   // plan, tables
+            S0 = sstep_uniform(&Sl);
+#ifdef FOTO_PLAN_CLOCK
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                foto_plan_clock[0] = c0;
+                foto_plan_clock[1] = c1;
+                foto_plan_clock[2] = wall_clock64();
+            }
+#endif
+        } else {
+            ring_stage_tables(T, tab);
+            __syncthreads();
+        }
+    } else {
+        ring_stage_tables(T, tab);
+        __syncthreads();
+    }
     double acc[NACC];
 #pragma unroll
     for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
-    const RingWave w = ring_wave(T, ring, D);
-    ring_pass<D, INIT>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, 0);
-    __shared__ double tot[NACC];
+    if (!LATE || !S0.done) ring_pass<D, INIT>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, issued);
+    else if (issued) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the prefetch
     if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
+    if constexpr (LATE) {
+        if (!S0.done)
+            for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[m] = tot[m];
+        if (threadIdx.x == 0) {
+            SStep So = S0;
+            So.pend = S0.done ? 0 : 1;
+            *Sg = So;
+        }
+        return;
+    }
     if (!FUSE) {
         for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
         return;
     }
     if (threadIdx.x >= 64) return;
-    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, INIT ? 1 : 0, rtol, maxiter);
 }
 
@@ -2105,6 +2189,8 @@ struct SpecImpl {
     std::vector<void*> allocs;
     int nblocks = 0;
     double c0 = 0, c1 = 1;
+
+    int late_plan() const { return (ring && world == 1 && !split_plan) ? 1 : 0; }   // k_spec_s2r LATE
 
     int alloc(size_t bytes, void** p) {
         FOTO_HIP_CHECK(hipMalloc(p, bytes));
@@ -2377,7 +2463,8 @@ static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* i
     // solve's pass count + 2, then chunks of 2.
     int passes = 0;
     (void)predicted;
-    const int first = P->last_passes > 0 ? P->last_passes + 2 : 8;
+    // (+1 with the ring's late planning: the plan that finds the solve done runs one launch later)
+    const int first = P->last_passes > 0 ? P->last_passes + 2 + P->late_plan() : 8;
     while (true) {
         const int chunk = (passes == 0) ? first : 2;
         for (int j = 0; j < chunk; ++j, ++passes) {
@@ -2478,7 +2565,7 @@ int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter,
     // FOTO_CG_MARGIN overrides the default 2 (tests force the redo path with a negative one)
     const char* me = getenv("FOTO_CG_MARGIN");
     const int margin = me ? atoi(me) : 2;
-    const int n = std::max(1, P->last_passes + margin);
+    const int n = std::max(1, P->last_passes + margin + P->late_plan());
     for (int j = 0; j < n; ++j) {
         hipEvent_t ep = kt ? kt->start(s) : nullptr;
         FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, nullptr, s));
