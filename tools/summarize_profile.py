@@ -91,6 +91,23 @@ def main():
         lines.append(f"| {n} | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.2f} | "
                      f"{float(r['AverageNs'])/1e3:.2f} | {float(r['MinNs'])/1e3:.2f} | "
                      f"{float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.2f} |")
+    # Working launches from the kernel trace: s-step passes launched past the end of a solve
+    # exit at once, and the pass whose plan finds the solve done only joins the ticket; launches
+    # under a quarter of the kernel's median are left out (bench.py's HIP-event timing drops
+    # the same launches), so "work avg" is comparable with the bench line's avg_launch_us.
+    tr = collections.defaultdict(list)
+    for r in csv.DictReader(open(find_csv(a.kt, "kernel_trace.csv"))):
+        tr[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    lines += ["", "## working launches (kernel trace; launches < 25 % of the median left out)", "",
+              "| kernel | working calls | work avg us | other calls | other avg us |", "|---|---|---|---|---|"]
+    for n, v in sorted(tr.items(), key=lambda t: -sum(t[1])):
+        med = sorted(v)[len(v) // 2]
+        wk = [x for x in v if x >= 0.25 * med]
+        ot = [x for x in v if x < 0.25 * med]
+        stats.setdefault(n, {})["work_avg_us"] = sum(wk) / len(wk)
+        stats[n]["work_calls"] = len(wk)
+        lines.append(f"| {n} | {len(wk)} | {sum(wk) / len(wk):.2f} | {len(ot)} | "
+                     f"{(sum(ot) / len(ot)) if ot else 0.0:.2f} |")
     traffic = {}
     fac_ld, fac_st = {8: 1.0, 16: 2.0}, 1.0   # defaults (guide); replaced by the calibration
     if a.calib_fetch and a.calib_write:
