@@ -131,8 +131,28 @@ __device__ __forceinline__ double row_L(const Geo& g, int t, int y, int x, doubl
 // barrier per plane).  Loads run one plane ahead of use.
 //   val(l, off)  -> field value at local plane l, in-plane offset off (in-domain only)
 //   body(l, t, off, x, y, c, xm, xp, ym, yp, tm, tp)   for in-domain voxels
+// Block -> tile for the column marches.  Workgroups are dispatched to the 8 XCDs round robin
+// (block b on XCD b % 8), each with its own L2; give every XCD a contiguous range of row-major
+// tiles instead, so the tile below a tile (ntx blocks later) is read through the same L2 and
+// the y-halo rows hit there instead of being fetched from HBM again (FOTO_XCD_SWIZZLE=0 in
+// the build: plain order, for A/B runs).
+#ifndef FOTO_XCD_SWIZZLE
+#define FOTO_XCD_SWIZZLE 1
+#endif
+__device__ __forceinline__ int xcd_tile(int b) {
+#if FOTO_XCD_SWIZZLE
+    constexpr int NXCD = 8;
+    const int nb = gridDim.x, per = nb / NXCD, rem = nb % NXCD;
+    const int xcd = b % NXCD, local = b / NXCD;
+    return xcd * per + min(xcd, rem) + local;
+#else
+    return b;
+#endif
+}
+
 template <class Val, class Body>
-__device__ __forceinline__ void march(const Geo& g, int tile, Val val, Body body) {
+__device__ __forceinline__ void march(const Geo& g, int tile_blk, Val val, Body body) {
+    const int tile = xcd_tile(tile_blk);
     constexpr int LW = TX + 2, LP = (TY + 2) * LW;
     __shared__ double lds[2 * LP];
     const int ntx = (g.Nx + TX - 1) / TX;
@@ -414,8 +434,9 @@ __global__ __launch_bounds__(RHS_NT) void k_rhs(Geo g, const double* __restrict_
     // t-field w_t = mu_t - r q_t of planes t-1, t, t+1 stays in registers (loaded one plane
     // ahead), the x / y fields' neighbours are same-row / adjacent-row loads (L1 / L2 hits).
     const int ntx = (g.Nx + TX - 1) / TX;
-    const int x = (blockIdx.x % ntx) * TX + (threadIdx.x & (TX - 1));
-    const int y = (blockIdx.x / ntx) * RHS_TY + threadIdx.x / TX;
+    const int tile = xcd_tile(blockIdx.x);
+    const int x = (tile % ntx) * TX + (threadIdx.x & (TX - 1));
+    const int y = (tile / ntx) * RHS_TY + threadIdx.x / TX;
     const bool in = x < g.Nx && y < g.Ny;
     const int64_t nxy = g.nxy, off = in ? (int64_t)y * g.Nx + x : 0;
     const bool has_lo = g.t0 > 0, has_hi = g.t0 + g.nloc < g.Nt;
