@@ -421,7 +421,7 @@ hipError_t launch_div_st(const Geo& g, const double* wt, const double* wx, const
 // F = div_st(mu - r q); F[t=0] -= rho0 - rho[0] + r a[0]; F[t=Nt-1] += rhoT - rho + r a
 // (benamou_brenier.py:64-82, dt = 1).  F.F partial -> gath[rank] (= b.b for CG).
 #ifndef FOTO_RHS_TY
-#define FOTO_RHS_TY 2
+#define FOTO_RHS_TY 1
 #endif
 constexpr int RHS_TY = FOTO_RHS_TY;    // rows per block: the y-neighbour rows a tile re-reads are 2 / RHS_TY extra
 constexpr int RHS_NT = TX * RHS_TY;
@@ -429,15 +429,20 @@ __global__ __launch_bounds__(RHS_NT) void k_rhs(Geo g, const double* __restrict_
                                             const double* __restrict__ muy, const double* __restrict__ qt,
                                             const double* __restrict__ qx, const double* __restrict__ qy,
                                             const double* __restrict__ rho0, const double* __restrict__ rhoT,
-                                            double r, double* __restrict__ F, RedBuf rb, double* gath, int rank) {
-    // one thread per (x, y) column of a 64 x 4 tile, marching over the shard's planes; the
-    // t-field w_t = mu_t - r q_t of planes t-1, t, t+1 stays in registers (loaded one plane
-    // ahead), the x / y fields' neighbours are same-row / adjacent-row loads (L1 / L2 hits).
-    const int ntx = (g.Nx + TX - 1) / TX;
-    const int tile = xcd_tile(blockIdx.x);
+                                            double r, double* __restrict__ F, RedBuf rb, double* gath, int rank,
+                                            int tch) {
+    // one thread per (x, y) column of a 64 x RHS_TY tile, marching over a chunk of tch of the
+    // shard's planes (chunks: more columns in flight than the 307 k of one full march, at the
+    // cost of re-reading the t-field of two planes per chunk); the t-field w_t = mu_t - r q_t
+    // of planes t-1, t, t+1 stays in registers (loaded one plane ahead), the x / y fields'
+    // neighbours are same-row / adjacent-row loads (L1 / L2 hits).
+    const int ntx = (g.Nx + TX - 1) / TX, ntiles = ntx * ((g.Ny + RHS_TY - 1) / RHS_TY);
+    const int lin = xcd_tile(blockIdx.x);
+    const int ch = lin / ntiles, tile = lin - ch * ntiles;
+    const int l0 = ch * tch, l1 = min(g.nloc, l0 + tch);
     const int x = (tile % ntx) * TX + (threadIdx.x & (TX - 1));
     const int y = (tile / ntx) * RHS_TY + threadIdx.x / TX;
-    const bool in = x < g.Nx && y < g.Ny;
+    const bool in = x < g.Nx && y < g.Ny && l0 < g.nloc;
     const int64_t nxy = g.nxy, off = in ? (int64_t)y * g.Nx + x : 0;
     const bool has_lo = g.t0 > 0, has_hi = g.t0 + g.nloc < g.Nt;
     auto wt = [&](int l) { const int64_t i = l * nxy + off; return mut[i] - r * qt[i]; };
@@ -445,11 +450,12 @@ __global__ __launch_bounds__(RHS_NT) void k_rhs(Geo g, const double* __restrict_
     auto wy = [&](int64_t i) { return muy[i] - r * qy[i]; };
     double ff = 0.0;
     if (in) {
-        double tm = has_lo ? wt(-1) : 0.0, tc = wt(0);
-        double tp = (g.nloc > 1 || has_hi) ? wt(1) : 0.0;
-        for (int l = 0; l < g.nloc; ++l) {
+        double tm = (l0 > 0 || has_lo) ? wt(l0 - 1) : 0.0, tc = wt(l0);
+        double tp = (l0 + 1 < g.nloc || has_hi) ? wt(l0 + 1) : 0.0;
+        for (int l = l0; l < l1; ++l) {
             const int t = g.t0 + l;
-            const double tpp = (l + 2 < g.nloc || (l + 2 == g.nloc && has_hi)) ? wt(l + 2) : 0.0;
+            const double tpp =
+                (l + 1 < l1 && (l + 2 < g.nloc || (l + 2 == g.nloc && has_hi))) ? wt(l + 2) : 0.0;
             const int64_t i = l * nxy + off;
             double s = 0.0;
             acc_d1w(s, t, g.Nt, tm, tc, tp);
@@ -472,8 +478,15 @@ __global__ __launch_bounds__(RHS_NT) void k_rhs(Geo g, const double* __restrict_
 hipError_t launch_rhs(const Geo& g, const double* mut, const double* mux, const double* muy, const double* qt,
                       const double* qx, const double* qy, const double* rho0, const double* rhoT, double r,
                       double* F, RedBuf rb, double* gath, int rank, hipStream_t s) {
-    const int nb = ((g.Nx + TX - 1) / TX) * ((g.Ny + RHS_TY - 1) / RHS_TY);
-    k_rhs<<<nb, RHS_NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb, gath, rank);
+    // planes per chunk (FOTO_RHS_TCH; default 8: four chunks at Nt = 32)
+    static const int tch = [] {
+        const char* e = getenv("FOTO_RHS_TCH");
+        const int v = e ? atoi(e) : 8;
+        return v > 0 ? v : 8;
+    }();
+    const int nch = (g.nloc + tch - 1) / tch;
+    const int nb = ((g.Nx + TX - 1) / TX) * ((g.Ny + RHS_TY - 1) / RHS_TY) * nch;
+    k_rhs<<<nb, RHS_NT, 0, s>>>(g, mut, mux, muy, qt, qx, qy, rho0, rhoT, r, F, rb, gath, rank, tch);
     return hipGetLastError();
 }
 
