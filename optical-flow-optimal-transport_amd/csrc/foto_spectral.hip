@@ -1372,6 +1372,14 @@ __device__ __forceinline__ double plan_mul_lam_dpp(double U, double c0, double c
 // ||r|| < atol, then p = beta p + r, alpha = rho / p.Ap, r -= alpha A p).  Called by all 64
 // lanes of one wave with the same S (state at the start of the pass) and the summed
 // moments tot[NACC] (shared); lane 0 stores the new state.
+#ifdef FOTO_PLAN_CLOCK   // timing studies only (tools/pass_lab.hip): 100 MHz stamps of block 0
+__device__ long long foto_plan_clock[8];
+#define FOTO_PLAN_STAMP(k) \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) foto_plan_clock[k] = wall_clock64()
+#else
+#define FOTO_PLAN_STAMP(k)
+#endif
+
 __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* xb /* shared, 3 NG + 2 */, int init,
                                 double rtol, int maxiter) {
     const int lane = threadIdx.x & 63;
@@ -1405,6 +1413,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
             hrow[c] = (lane < NG && ia + ic < NMOM) ? 0.5 * (M[ia + ic] + M[ia > ic ? ia - ic : ic - ia]) : 0.0;
         }
     }
+    FOTO_PLAN_STAMP(3);
     double R = (lane == 0) ? 1.0 : 0.0;     // r_k     = 1 * r
     double P = (lane == NCO) ? 1.0 : 0.0;   // p_{k-1} = 1 * q
     double rho_prev = S.rho_prev;
@@ -1450,6 +1459,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         }
         ++n;
     }
+    FOTO_PLAN_STAMP(4);
     S.nsteps = n;
     S.rho_prev = rho_prev;
     S.passes += 1;
@@ -1505,6 +1515,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         }
     }
     if (adapt && !projected && mom_var >= 0.0) to_interval(mom_mean, mom_var, nc0, nc1);
+    FOTO_PLAN_STAMP(5);
     if (lane == 0) {   // scalars only: a[], b[] were stored above
         Sg->k = S.k; Sg->nsteps = S.nsteps; Sg->fin = S.fin; Sg->conv = S.conv; Sg->done = S.done;
         Sg->iters = S.iters; Sg->passes = S.passes; Sg->rho_prev = S.rho_prev; Sg->atol = S.atol;
@@ -1852,10 +1863,6 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
         }
     }
 }
-
-#ifdef FOTO_PLAN_CLOCK
-__device__ long long foto_plan_clock[4];
-#endif
 
 // SStep from LDS into wave-uniform registers (the plan made in LDS feeds the step loop's
 // scalar operands)

@@ -164,10 +164,12 @@ int main() {
         printf("%-44s %6.1f us (single launch; %d steps, pend %d)\n", "ring D=4 fused plan (at start)", best * 1e3,
                hS.nsteps, hS.pend);
 #ifdef FOTO_PLAN_CLOCK
-        long long ck[4];
+        long long ck[8];
         (void)hipMemcpyFromSymbol(ck, HIP_SYMBOL(foto_plan_clock), sizeof ck);
         printf("   block 0 wave 0: moments load + plan %.2f us, then barrier %.2f us\n", (ck[1] - ck[0]) * 0.01,
                (ck[2] - ck[1]) * 0.01);
+        printf("   plan: to Gram rows %.2f us, steps %.2f us, interval %.2f us, stores %.2f us\n",
+               (ck[3] - ck[0]) * 0.01, (ck[4] - ck[3]) * 0.01, (ck[5] - ck[4]) * 0.01, (ck[1] - ck[5]) * 0.01);
 #endif
     }
     if (hipDeviceSynchronize() != hipSuccess) return 2;
