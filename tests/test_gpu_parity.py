@@ -222,6 +222,32 @@ def test_bb_deferred_cg(gold, monkeypatch, env):
         assert st["cg_redo"] == 0
 
 
+def test_bb_cg_maxiter_deferred(gold, monkeypatch):
+    """Outer iterations whose CG stops at maxiter (info = maxiter, as scipy reports it), 7 CG
+    iterations each.  The deferred single-shard solve (late-planned passes, prox behind the done
+    flag) reproduces the solve waited for on the host bit for bit, and the one-iteration-per-
+    pass spectral CG to 1e-8.  (Truncated CG iterates are rounding-sensitive: at 7 iterations
+    the spectral phi is 5.5e-10 from scipy's and the stencil phi 3e-12, which the prox turns
+    into 1e-7 .. 5e-5 in crit over six outer iterations; at 20 iterations the phi differences
+    are 4.6e-4 / 1.7e-6, measured against the oracle on this golden -- converged solves meet the
+    goldens.)"""
+    d = gold("bb_c1.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, _, eps, _ = d["params"]
+    res = {}
+    for key, mode, defer in (("s1", 1, "1"), ("s2", 2, "1"), ("s2_wait", 2, "0")):
+        monkeypatch.setenv("FOTO_CG_DEFER", defer)
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode, cg_maxiter=7) as s:
+            s.iterate(6, 0.0, False)
+            res[key] = (np.array(s.crit), np.array(s.cg_its), np.array(s.cg_info), s.flow(), s.stats())
+    for c, k, i, _, st in res.values():
+        assert np.all(k == 7) and np.all(i == 7) and st["cg_redo"] == 0
+    assert np.array_equal(res["s2"][0], res["s2_wait"][0])
+    for a, b in zip(res["s2"][3], res["s2_wait"][3]):
+        assert np.array_equal(a, b)
+    np.testing.assert_allclose(res["s2"][0], res["s1"][0], rtol=1e-8, atol=0)
+
+
 @pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("vr", [2, 3, 5])
 def test_bb_virtual_ranks_match_single(gold, vr, mode):
