@@ -1877,8 +1877,10 @@ __device__ __forceinline__ SStep sstep_uniform(const SStep* p) {
     return s;
 }
 
-// FUSE (single shard): a working pass plans itself.  The pass that takes the moments leaves
-// them in gath with S.pend = 1; the next pass's blocks each make that plan at their start
+// FUSE (working passes): a pass plans itself.  The pass that takes the moments leaves them in
+// gath (this rank's slot; between passes of a sharded solve the all-gather fills the others)
+// with S.pend = 1; the next pass's blocks each make that plan at their start, from the slots
+// summed in rank order (as k_spec_s2_plan sums them, so every rank plans identically)
 // (wave 0, identical inputs and code, so identical plans) while the other waves' first ring
 // tiles are already loading, instead of one block planning in the tail of the previous pass
 // with the whole chip idle behind it.  The last block (ticket) publishes the new moments and
@@ -1888,7 +1890,7 @@ __device__ __forceinline__ SStep sstep_uniform(const SStep* p) {
 template <int D, bool INIT, bool FUSE>
 __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_spec_s2r(
         SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
-        RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
+        RedBuf rb, double rtol, int maxiter, double* gath, int rank, int world) {
     constexpr bool LATE = FUSE && !INIT;
     __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
     __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
@@ -1913,7 +1915,11 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
             const long long c0 = wall_clock64();
 #endif
             if (threadIdx.x < 64) {
-                if (threadIdx.x < NACC) tot[threadIdx.x] = gath[threadIdx.x];
+                if (threadIdx.x < NACC) {   // the ranks' moments, summed in rank order (k_spec_s2_plan's)
+                    double t = 0.0;
+                    for (int g = 0; g < world; ++g) t += gath[g * NACC + threadIdx.x];
+                    tot[threadIdx.x] = t;
+                }
                 if (threadIdx.x == 0) Sl = S0;
                 FOTO_LDS_WAIT();
                 for (int j = 0; j < issued; ++j) ring_issue<D>(T, w, j, src, ph, k > 0);
@@ -1949,8 +1955,8 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
     else if (issued) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the prefetch
     if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
     if constexpr (LATE) {
-        if (!S0.done)
-            for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[m] = tot[m];
+        if (!S0.done)   // this rank's slot (the all-gather between passes fills the others)
+            for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
         if (threadIdx.x == 0) {
             SStep So = S0;
             So.pend = S0.done ? 0 : 1;
@@ -1972,9 +1978,10 @@ static_assert(ring_fits(FOTO_RING_D), "ring + tables exceed the LDS");
 // host launcher (D = 0: FOTO_RING_D)
 static hipError_t launch_s2_ring(const SpecTab& T, double* rh, double* ph, const double* bh, SStep* Sg, RedBuf rb,
                                  double rtol, int maxiter, double* gath, int rank, bool init, bool fuse, int D,
-                                 int nb = 256, hipStream_t s = 0) {
+                                 int nb = 256, hipStream_t s = 0, int world = 1) {
     if (D == 0) D = FOTO_RING_D;
-#define FOTO_RL(DD, I, F) k_spec_s2r<DD, I, F><<<nb, S2_NTH, 0, s>>>(T, rh, ph, bh, Sg, rb, rtol, maxiter, gath, rank)
+#define FOTO_RL(DD, I, F) \
+    k_spec_s2r<DD, I, F><<<nb, S2_NTH, 0, s>>>(T, rh, ph, bh, Sg, rb, rtol, maxiter, gath, rank, world)
 #define FOTO_RL_D(DD)                                                                        \
     if (D == DD) {                                                                           \
         if constexpr (ring_fits(DD)) {                                                       \
@@ -2197,7 +2204,9 @@ struct SpecImpl {
     int nblocks = 0;
     double c0 = 0, c1 = 1;
 
-    int late_plan() const { return (ring && world == 1 && !split_plan) ? 1 : 0; }   // k_spec_s2r LATE
+    // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
+    // sharded always), so the plan that finds a solve done runs one launch later
+    int late_plan() const { return (ring && (world > 1 || !split_plan)) ? 1 : 0; }
 
     int alloc(size_t bytes, void** p) {
         FOTO_HIP_CHECK(hipMalloc(p, bytes));
@@ -2706,17 +2715,24 @@ int SpectralPlan::cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s) 
 int SpectralPlan::cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, P->gath, s));
+    if (P->late_plan())   // plans at its start from the all-gathered moments (no cg_plan after it)
+        FOTO_HIP_CHECK(launch_s2_ring(P->tab(), P->rh, P->ph, P->bh, P->S2, P->rb, rtol, maxiter, P->gath, P->rank,
+                                      false, true, FOTO_RING_D, P->nb_ring, s, P->world));
+    else
+        FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, P->gath, s));
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * P->nbox());
     return 0;
 }
 
 int SpectralPlan::cg_plan(int init, double rtol, int maxiter, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
+    if (!init && P->late_plan()) return 0;   // the next cg_pass plans at its start
     k_spec_s2_plan<<<1, 64, 0, s>>>(P->S2, P->gath, P->world, init, rtol, maxiter);
     FOTO_HIP_CHECK(hipGetLastError());
     return 0;
 }
+
+int SpectralPlan::late_extra() const { return ((const SpecImpl*)impl)->late_plan(); }
 
 int SpectralPlan::poll(int* done, int* iters, int* passes, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
