@@ -71,11 +71,13 @@ struct Shard {
         allocs.push_back(*out);
         return 0;
     }
-    int alloc_field(double** out) {   // (nloc + 2) planes, zeroed
+    // (nloc + 2) planes, zeroed on the context's stream: a hipMemset (null stream) is not
+    // ordered with the non-blocking stream the kernels run on -- it raced with k_init_mu
+    int alloc_field(double** out, hipStream_t st) {
         void* b = nullptr;
         const size_t n = (size_t)(g.nloc + 2) * (size_t)g.nxy;
         FOTO_TRY(alloc(n * sizeof(double), &b));
-        FOTO_HIP_CHECK(hipMemset(b, 0, n * sizeof(double)));
+        FOTO_HIP_CHECK(hipMemsetAsync(b, 0, n * sizeof(double), st));
         *out = (double*)b + g.nxy;
         return 0;
     }
@@ -110,6 +112,9 @@ struct foto_bb_ctx {
     double* hgath = nullptr;                  // pinned host mirror of gath
     int last_cg = 0;
     int last_passes = 0;   // s-step passes of the previous sharded spectral solve
+    // the outer iteration on the stream (outer_enqueue -> outer_complete)
+    int enq_its = 0, enq_info = 0;
+    SpectralPlan* enq_dsp = nullptr;
     int have_phi = 0;
     // bookkeeping
     double prev_crit = -1;
@@ -207,11 +212,11 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
             set_error("world size %d exceeds Nt = %d (each rank needs >= 1 time slab)", W, c->Nt);
             return FOTO_ERR_ARG;
         }
-        for (int f = 0; f < 3; ++f) { FOTO_TRY(s.alloc_field(&s.mu[f])); FOTO_TRY(s.alloc_field(&s.q[f])); }
-        FOTO_TRY(s.alloc_field(&s.phi));
-        FOTO_TRY(s.alloc_field(&s.rv));
-        FOTO_TRY(s.alloc_field(&s.p[0]));
-        FOTO_TRY(s.alloc_field(&s.p[1]));
+        for (int f = 0; f < 3; ++f) { FOTO_TRY(s.alloc_field(&s.mu[f], c->s)); FOTO_TRY(s.alloc_field(&s.q[f], c->s)); }
+        FOTO_TRY(s.alloc_field(&s.phi, c->s));
+        FOTO_TRY(s.alloc_field(&s.rv, c->s));
+        FOTO_TRY(s.alloc_field(&s.p[0], c->s));
+        FOTO_TRY(s.alloc_field(&s.p[1], c->s));
         void* b;
         FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.rho0 = (double*)b;
         FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.rhoT = (double*)b;
@@ -224,9 +229,9 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         s.rb.cap = (int)(2 * nb);
         FOTO_TRY(s.alloc(sizeof(double) * s.rb.cap, &b)); s.rb.partials = (double*)b;
         FOTO_TRY(s.alloc(sizeof(unsigned) * 64, &b)); s.rb.ticket = (unsigned*)b;
-        FOTO_HIP_CHECK(hipMemset(s.rb.ticket, 0, sizeof(unsigned) * 64));
+        FOTO_HIP_CHECK(hipMemsetAsync(s.rb.ticket, 0, sizeof(unsigned) * 64, c->s));
         FOTO_TRY(s.alloc(sizeof(double) * 4 * W, &b)); s.gath = (double*)b;
-        FOTO_HIP_CHECK(hipMemset(s.gath, 0, sizeof(double) * 4 * W));
+        FOTO_HIP_CHECK(hipMemsetAsync(s.gath, 0, sizeof(double) * 4 * W, c->s));
         FOTO_TRY(s.alloc(sizeof(CGScal), &b)); s.S = (CGScal*)b;
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rho0, rho0, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rhoT, rhoT, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
@@ -421,8 +426,15 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 
 // ----------------------------------------------------------------------------- outer iteration
 
-static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_info) {
+// One outer iteration in two halves.  outer_enqueue puts the iteration's work on the stream
+// (a non-deferred CG solve waits for itself inside); outer_complete waits for the crit
+// readback, finishes a deferred solve and computes crit.  foto_bb_iterate enqueues the next
+// iteration as soon as the stop rules have seen crit, and only then resolves the kernel timers
+// and calls the host callback, so that host work overlaps the GPU.
+static int outer_enqueue(foto_bb_ctx* c) {
     const int W = c->W;
+    int* cg_iters = &c->enq_its;
+    int* cg_info = &c->enq_info;
     FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
     FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
     FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
@@ -469,6 +481,16 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
     FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
     FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
+    c->enq_dsp = dsp;
+    return 0;
+}
+
+static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_info) {
+    const int W = c->W;
+    SpectralPlan* dsp = c->enq_dsp;
+    c->enq_dsp = nullptr;
+    *cg_iters = c->enq_its;
+    *cg_info = c->enq_info;
     FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
     if (dsp) {
         int redo = 0;
@@ -495,7 +517,6 @@ static int outer_iteration(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_
     c->st.ms_rhs += t_rhs;
     c->st.ms_cg += t_cg;
     c->st.ms_prox += t_prox;
-    c->kt.resolve();
 
     double num = 0.0, den = 0.0;
     for (int g = 0; g < W; ++g) { num += c->hgath[2 * W + 2 * g]; den += c->hgath[2 * W + 2 * g + 1]; }
@@ -658,18 +679,24 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
     int done = 0;
     int stopped = 0;
+    if (max_iters > 0) FOTO_TRY(outer_enqueue(c));
     for (int i = 0; i < max_iters; ++i) {
         double crit;
         int its, info;
-        FOTO_TRY(outer_iteration(c, &crit, &its, &info));
+        FOTO_TRY(outer_complete(c, &crit, &its, &info));
         ++done;
-        if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
         const double prev = c->prev_crit;
         c->prev_crit = crit;
         if (use_stop_rules) {
-            if (crit <= tol) { stopped = 1; break; }
-            if (prev >= 0 && std::fabs(prev - crit) < 1e-5) { stopped = 1; break; }
+            if (crit <= tol) stopped = 1;
+            else if (prev >= 0 && std::fabs(prev - crit) < 1e-5) stopped = 1;
         }
+        // the next iteration goes on the stream before the host's bookkeeping for this one
+        const size_t mark = c->kt.pending();
+        if (!stopped && i + 1 < max_iters) FOTO_TRY(outer_enqueue(c));
+        c->kt.resolve_first(mark);
+        if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
+        if (stopped) break;
     }
     if (iters_done) *iters_done = done;
     return stopped;

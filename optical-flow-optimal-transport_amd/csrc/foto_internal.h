@@ -110,6 +110,23 @@ struct KTimer {
             --count;
         }
     }
+    size_t pending() const { return pend.size(); }
+    // the first n pending intervals (all complete: recorded before the last stream sync)
+    void resolve_first(size_t n) {
+        n = std::min(n, pend.size());
+        for (size_t k = 0; k < n; ++k) {
+            Pend& p = pend[k];
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+                this->n[p.cls] += 1;
+                ms[p.cls] += t;
+                bytes[p.cls] += p.bytes;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pend.erase(pend.begin(), pend.begin() + n);
+    }
     void resolve() {   // call after a stream sync
         for (auto& p : pend) {
             float t = 0.f;

@@ -2368,7 +2368,7 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     P->rb.partials = (double*)b;
     P->rb.ticket = (unsigned*)((double*)b + cap);
     P->rb.cap = cap;
-    FOTO_HIP_CHECK(hipMemset(P->rb.ticket, 0, 8 * sizeof(double)));
+    FOTO_HIP_CHECK(hipMemsetAsync(P->rb.ticket, 0, 8 * sizeof(double), s));
     FOTO_TRY(P->alloc(sizeof(double) * std::max(4, NACC * world), &b)); P->gath = (double*)b;
     FOTO_TRY(P->alloc(sizeof(CGScal), &b)); P->S = (CGScal*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
