@@ -121,12 +121,15 @@ struct foto_bb_ctx {
     foto_bb_stats st{};
     KTimer kt;
     hipEvent_t ph[4] = {nullptr, nullptr, nullptr, nullptr};   // phase boundaries (rhs | cg | prox)
+    hipEvent_t phr[2] = {nullptr, nullptr};   // RHS start, by parity (the next RHS may be enqueued early)
+    int hpar = 0, tail_par = 0;
     ~foto_bb_ctx() {
         sh.clear();
         if (nc) (void)ncclCommDestroy(nc);
         if (hS) (void)hipHostFree(hS);
         if (hgath) (void)hipHostFree(hgath);
         for (auto e : ph) if (e) (void)hipEventDestroy(e);
+        for (auto e : phr) if (e) (void)hipEventDestroy(e);
         if (s) (void)hipStreamDestroy(s);
     }
 };
@@ -197,6 +200,7 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     const int W = c->W;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hgath, sizeof(double) * 4 * W));
     for (auto& e : c->ph) FOTO_HIP_CHECK(hipEventCreate(&e));
+    for (auto& e : c->phr) FOTO_HIP_CHECK(hipEventCreate(&e));
     if (c->rccl) {
         ncclUniqueId id;
         memcpy(&id, c->o.nccl_id, sizeof(id));
@@ -428,14 +432,15 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 
 // One outer iteration in two halves.  outer_enqueue puts the iteration's work on the stream
 // (a non-deferred CG solve waits for itself inside); outer_complete waits for the crit
-// readback, finishes a deferred solve and computes crit.  foto_bb_iterate enqueues the next
-// iteration as soon as the stop rules have seen crit, and only then resolves the kernel timers
-// and calls the host callback, so that host work overlaps the GPU.
-static int outer_enqueue(foto_bb_ctx* c) {
-    const int W = c->W;
-    int* cg_iters = &c->enq_its;
-    int* cg_info = &c->enq_info;
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+// readback, finishes a deferred solve and computes crit.  The enqueue half is itself split:
+// outer_head (halos, RHS) only writes F and, for a single spectral shard, foto_bb_iterate
+// puts the next iteration's head on the stream before waiting for this iteration's crit, so
+// the GPU computes the RHS while the host wakes up (the stop rules can still end the run there:
+// F is scratch; a CG redo re-runs the head).  The host callback runs after the next
+// iteration is enqueued.
+static int outer_head(foto_bb_ctx* c) {
+    c->hpar ^= 1;
+    FOTO_HIP_CHECK(hipEventRecord(c->phr[c->hpar], c->s));
     FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
     FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
     for (auto& sp : c->sh) {
@@ -447,6 +452,14 @@ static int outer_enqueue(foto_bb_ctx* c) {
         c->kt.stop(e, c->s, FOTO_K_RHS, 56.0 * nv);
     }
     if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    return 0;
+}
+
+static int outer_tail(foto_bb_ctx* c) {
+    const int W = c->W;
+    int* cg_iters = &c->enq_its;
+    int* cg_info = &c->enq_info;
+    c->tail_par = c->hpar;
     // phase boundaries are recorded, not waited on: the one host wait per outer iteration
     // is the crit readback below (a wait here idled the GPU for the host's wake-up)
     FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
@@ -511,7 +524,7 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
         }
     }
     float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->ph[0], c->ph[1]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->phr[c->tail_par], c->ph[1]));
     FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[1], c->ph[2]));
     FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, c->ph[2], c->ph[3]));
     c->st.ms_rhs += t_rhs;
@@ -679,10 +692,19 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
     int done = 0;
     int stopped = 0;
-    if (max_iters > 0) FOTO_TRY(outer_enqueue(c));
+    // the next RHS goes on the stream early for a single spectral shard (see outer_head)
+    const bool early = c->W == 1 && c->o.cg_mode != 0;
+    if (max_iters > 0) {
+        FOTO_TRY(outer_head(c));
+        FOTO_TRY(outer_tail(c));
+    }
     for (int i = 0; i < max_iters; ++i) {
         double crit;
         int its, info;
+        const size_t mark = c->kt.pending();
+        const bool head_early = early && i + 1 < max_iters;
+        if (head_early) FOTO_TRY(outer_head(c));
+        const int redo0 = c->st.cg_redo;
         FOTO_TRY(outer_complete(c, &crit, &its, &info));
         ++done;
         const double prev = c->prev_crit;
@@ -692,8 +714,11 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
             else if (prev >= 0 && std::fabs(prev - crit) < 1e-5) stopped = 1;
         }
         // the next iteration goes on the stream before the host's bookkeeping for this one
-        const size_t mark = c->kt.pending();
-        if (!stopped && i + 1 < max_iters) FOTO_TRY(outer_enqueue(c));
+        if (!stopped && i + 1 < max_iters) {
+            // a redo re-ran this iteration's prox after the early head read mu, q: head again
+            if (!head_early || c->st.cg_redo != redo0) FOTO_TRY(outer_head(c));
+            FOTO_TRY(outer_tail(c));
+        }
         c->kt.resolve_first(mark);
         if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
         if (stopped) break;
