@@ -1419,6 +1419,9 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
     double rho_prev = S.rho_prev;
     int n = 0;
     bool conv = false;
+    double av = 0.0, bv = 0.0;   // lane i: step i's alpha, beta (stored after the loop)
+    // wave-uniform tests as scalar branches (the values are uniform; the compiler cannot see it)
+    auto uni = [](bool b) { return __builtin_amdgcn_readfirstlane(b ? 1 : 0) != 0; };
 #pragma clang loop unroll(full)
     for (int i = 0; i < SMAX; ++i) {
         if (S.k + i >= maxiter) break;
@@ -1432,9 +1435,9 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
 #else
             rho = plan_ip(R, R, hrow, xb, &cr);
 #endif
-            if (!(cr <= 1.0)) break;   // badly conditioned (or NaN): leave it to the next pass
+            if (uni(!(cr <= 1.0))) break;   // badly conditioned (or NaN): leave it to the next pass
         }
-        if (rho == 0.0 || sqrt(rho) < S.atol) { conv = true; break; }
+        if (uni(rho == 0.0 || sqrt(rho) < S.atol)) { conv = true; break; }
         const bool first = (S.k + i == 0);
         const double beta = first ? 0.0 : rho / rho_prev;
         const double Pn = first ? R : beta * P + R;
@@ -1448,16 +1451,18 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         const double Q = plan_mul_lam(Pn, S.c0, S.c1, xb);
         const double den = plan_ip(Pn, Q, hrow, xb, &cr);
 #endif
-        if (i > 0 && !(cr <= 1.0)) break;
+        if (i > 0 && uni(!(cr <= 1.0))) break;
         const double alpha = rho / den;
         R = R - alpha * Q;
         P = Pn;
         rho_prev = rho;
-        if (lane == 0) {
-            Sg->a[i] = alpha;
-            Sg->b[i] = beta;
-        }
+        av = (lane == i) ? alpha : av;
+        bv = (lane == i) ? beta : bv;
         ++n;
+    }
+    if (lane < n) {
+        Sg->a[lane] = av;
+        Sg->b[lane] = bv;
     }
     FOTO_PLAN_STAMP(4);
     S.nsteps = n;
