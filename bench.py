@@ -106,7 +106,7 @@ def gn_side(with_cpu):
     from foto import gn
     from foto.synthetic import sinusoid_pair
     out = {"workload": f"GN classical solve, sinusoid pair, alpha={GN_ALPHA}, lambda={GN_LAMBDA}, "
-                       f"block-Jacobi PCG to rtol {gn.GN_RTOL}"}
+                       f"CG preconditioned by a symmetric multigrid V-cycle (FOTO_GN_MG=0: block-Jacobi) to rtol {gn.GN_RTOL}"}
     for (w, h) in ((GN_W, GN_H), (GN_CPU_W, GN_CPU_H)):
         f1, f2 = sinusoid_pair(w, h)
         best = None
