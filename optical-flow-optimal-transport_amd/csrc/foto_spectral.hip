@@ -1161,8 +1161,8 @@ __global__ __launch_bounds__(NT) void k_spec_xhat(SpecTab T, const double* __res
 // B_i(lam) q with Chebyshev-coefficient polynomials, inner products through the Gram matrix
 // (M_{a+c} + M_{|a-c|}) / 2.  Step i > 0 is taken only while its two Gram-form inner
 // products (rho_{k+i} and p.Ap) are well conditioned: sum |terms| / |result| <= S_CLIM
-// (1e4, i.e. ~1e-12 relative rounding).  Early in a solve the residual measure is a few
-// dominant low-frequency components, the Chebyshev-Krylov basis is nearly degenerate and
+// (3e4, i.e. ~3e-12 relative rounding; DESIGN.md 3.1.1 has the sweep).  Early in a solve
+// the residual measure is a few dominant low-frequency components, the Chebyshev-Krylov basis is nearly degenerate and
 // passes take 1-2 steps; later ones take SMAX.  A fixed s >= 3 loses digits in the first
 // passes (measured: alpha off by 1e-4 at s = 3, k = 0).  tests/test_sstep_plan.py checks
 // the planning rule (numpy restatement) against the golden solves: the same CG counts as
@@ -1176,7 +1176,10 @@ constexpr int NMOM = 2 * SMAX;       // moments per family: degrees 0 .. 2 SMAX 
 constexpr int NACC = 3 * NMOM;       // rr, rq, qq
 constexpr int NCO = SMAX + 1;        // Chebyshev coefficients per part (degree <= SMAX)
 constexpr int NG = 2 * NCO;          // combined (r part, q part) coefficient index
-constexpr double S_CLIM = 1e4;       // cancellation limit of a Gram-form inner product
+#ifndef FOTO_S_CLIM
+#define FOTO_S_CLIM 3e4
+#endif
+constexpr double S_CLIM = FOTO_S_CLIM;   // cancellation limit of a Gram-form inner product
 static_assert(NG <= 64, "coefficients live one per lane");
 
 struct SStep {

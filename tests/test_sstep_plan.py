@@ -8,7 +8,7 @@ the residual measure ([lmin, mean + 2 sd]: of b^ of the previous solve for the I
 the whole spectrum for a run's first solve; of the new residual, projected through the Gram,
 after short passes; of the pass-start state otherwise); step i > 0 is taken only
 while its two Gram-form inner products have cancellation ratio sum|terms| / |value| <=
-S_CLIM = 1e4, and the moments are summed with compensated block reductions (correctly
+S_CLIM = 3e4, and the moments are summed with compensated block reductions (correctly
 rounded to ~1 ulp).  This module restates that rule on the CPU (test infrastructure: the
 oracle provides the rhs, the goldens the reference's answers) and checks that it keeps
 scipy's CG iteration counts and the reference's crit / iterate to the stated bars.  The
@@ -28,7 +28,7 @@ from oracle import foto_oracle as O  # noqa: E402
 SMAX = 8
 NMOM = 2 * SMAX
 NCO = SMAX + 1
-S_CLIM = 1e4
+S_CLIM = 3e4
 S_KAPPA = 2.0
 S_PROJ = (NMOM - 3) // 2   # projected interval after n <= S_PROJ steps
 
