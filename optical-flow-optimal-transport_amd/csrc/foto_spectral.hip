@@ -1210,7 +1210,10 @@ struct SStep {
 // accurate regardless.  Measured (numpy restatement, tests/test_sstep_plan.py): at the bench
 // grid 24 -> 22 passes on the first outer iteration, 33 -> 28 at 160x120x32; no change in
 // CG counts or iterates.
-constexpr double S_KAPPA = 2.0;
+#ifndef FOTO_S_KAPPA
+#define FOTO_S_KAPPA 2.0
+#endif
+constexpr double S_KAPPA = FOTO_S_KAPPA;
 constexpr int S_PROJ = (NMOM - 3) / 2;   // projected interval after n <= S_PROJ steps (2n + 2 < NMOM)
 
 // Plan helpers.  Coefficient vectors are distributed one entry per lane: lane j < NG holds
