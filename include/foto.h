@@ -60,7 +60,8 @@ int foto_bb_rhs(const double* mu3, const double* q3, const double* rho0, const d
                 int Nt, int Nx, int Ny, double r, double* F);
 /* scipy.sparse.linalg.cg(A, b, rtol, maxiter) with A = -r L_st + r eps I, x0 = 0
  * (benamou_brenier.py:85).  Returns info (0 converged, maxiter otherwise) or < 0;
- * *iterations = CG iterations run.  mode: 0 = stencil CG, 1 = spectral CG.        */
+ * *iterations = CG iterations run.  mode: 0 = stencil CG, 1 = spectral CG,
+ * 2 = spectral s-step CG (the foto_bb_opts.cg_mode values).                        */
 int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double eps, double rtol, int maxiter,
             int mode, double* x, int* iterations);
 /* utils.opticalflow_from_benamoubrenier(phi, Nt, Nx, Ny, grad('N'), div('D'))
