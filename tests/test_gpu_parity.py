@@ -397,3 +397,20 @@ def test_gn_solve(gold):
         assert info == 0 and its > 0
         for a, b in ((u, d[f"n{g}_u"]), (v, d[f"n{g}_v"]), (m, d[f"n{g}_m"])):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("pair", ["sinusoid", "textured"])
+def test_gn_solve_multilevel(pair, monkeypatch):
+    """GN at 160x120 -- a four-level V-cycle (160x120 .. 20x15), which the goldens (40x30,
+    17x13: two levels / coarse solve only) do not reach -- against the oracle's spsolve
+    (SuperLU, classical.py:126), with the graph-replayed and the directly launched iteration."""
+    from foto.synthetic import sinusoid_pair, textured_pair
+    w, h, alpha, lam = 160, 120, 0.1, 0.2
+    f1, f2 = (sinusoid_pair if pair == "sinusoid" else textured_pair)(w, h)
+    ref = O.gn_solve(f1, f2, w, h, alpha, lam)
+    for graph in ("1", "0"):
+        monkeypatch.setenv("FOTO_GN_GRAPH", graph)
+        u, v, m, info, its = gn.solve(f1, f2, w, h, alpha, lam)
+        assert info == 0 and 0 < its < 100
+        for a, b in zip((u, v, m), ref):
+            np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * max(1.0, np.abs(b).max()))
