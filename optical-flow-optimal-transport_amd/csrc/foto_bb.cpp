@@ -363,7 +363,7 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));
     int passes = 0, done = 0, its = 0, planned = 0;
-    const int first = c->last_passes > 0 ? c->last_passes + 2 + c->sh[0]->spec->late_extra() : 8;   // over-predict (see solve_s2)
+    const int first = c->last_passes > 0 ? c->last_passes + 2 : 8;   // over-predict (see solve_s2)
     while (true) {
         const int chunk = (passes == 0) ? first : 2;
         for (int j = 0; j < chunk; ++j, ++passes) {

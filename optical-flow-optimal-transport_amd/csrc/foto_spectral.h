@@ -28,7 +28,6 @@ struct SpectralPlan {
     int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // planned CG steps, moments -> gath
     int cg_plan(int init, double rtol, int maxiter, hipStream_t s);      // after the all-gather
     int poll(int* done, int* iters, int* passes, hipStream_t s);
-    int late_extra() const;   // 1: passes plan at their start; the done-finding plan is one launch later
     int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
     int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // unpack stage, inverse y, x
     double* stage() const;     // physical-side all-to-all buffer [h][tl][rows of h][x]

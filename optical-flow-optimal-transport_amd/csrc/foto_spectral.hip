@@ -1783,7 +1783,8 @@ __device__ __forceinline__ void ring_issue(const SpecTab& T, const RingWave& w, 
 template <int D, bool INIT>
 __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, unsigned tab_a, const SStep& S0,
                                           double* __restrict__ rh, double* __restrict__ ph,
-                                          const double* __restrict__ bh, double (&acc)[NACC], int issued) {
+                                          const double* __restrict__ bh, double (&acc)[NACC], int issued,
+                                          bool mom = true) {
     const int lane = threadIdx.x & 63;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
     const double c0 = INIT ? S0.ic0 : S0.c0, ic1 = 1.0 / (INIT ? S0.ic1 : S0.c1);
@@ -1864,7 +1865,7 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
                 *reinterpret_cast<dbl2*>(ph + i) = dbl2{q0, q1};
             }
         }
-        if (ok) {
+        if (ok && mom) {
 #if defined(FOTO_RING_ABLATE)   // timing studies only (tools/pass_lab.hip): no moments
             acc[0] += r0 * q0 + r1 * q1 + l0 * l1;
 #else
@@ -1895,9 +1896,10 @@ __device__ __forceinline__ SStep sstep_uniform(const SStep* p) {
 // (wave 0, identical inputs and code, so identical plans) while the other waves' first ring
 // tiles are already loading, instead of one block planning in the tail of the previous pass
 // with the whole chip idle behind it.  The last block (ticket) publishes the new moments and
-// state once every block has read the old ones.  A plan that finds the solve done still
-// passes the ticket, so that one block stores the final state.  INIT passes plan in their
-// tail (the fused t-DCT INIT and the ring INIT pass), leaving pend = 0.
+// state once every block has read the old ones.  The pass whose plan finishes the solve (fin)
+// skips the moments and its last block marks the solve done; a plan that finds the solve done
+// at once (no step left) still passes the ticket, so that one block stores the final state.
+// INIT passes plan in their tail (the fused t-DCT INIT and the ring INIT pass), leaving pend = 0.
 template <int D, bool INIT, bool FUSE>
 __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_spec_s2r(
         SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, SStep* Sg,
@@ -1962,15 +1964,25 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
     double acc[NACC];
 #pragma unroll
     for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
-    if (!LATE || !S0.done) ring_pass<D, INIT>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, issued);
+    // the pass whose plan finished the solve (fin) needs no moments: its tail marks the solve
+    // done (the bookkeeping sstep_plan_wave's fin branch would do at the next pass's start)
+    const bool final_pass = LATE && S0.fin && !S0.done;
+    if (!LATE || !S0.done) ring_pass<D, INIT>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, issued, !final_pass);
     else if (issued) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the prefetch
     if (!sp_reduce_last_rs<NACC, S2_NTH>(acc, rb, tot)) return;
     if constexpr (LATE) {
-        if (!S0.done)   // this rank's slot (the all-gather between passes fills the others)
+        if (!S0.done && !final_pass)   // this rank's slot (the all-gather between passes fills the others)
             for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
         if (threadIdx.x == 0) {
             SStep So = S0;
-            So.pend = S0.done ? 0 : 1;
+            if (final_pass) {
+                So.k += So.nsteps;
+                So.done = So.conv ? 1 : 2;
+                So.nsteps = 0;
+                So.pend = 0;
+            } else {
+                So.pend = S0.done ? 0 : 1;
+            }
             *Sg = So;
         }
         return;
@@ -2216,7 +2228,7 @@ struct SpecImpl {
     double c0 = 0, c1 = 1;
 
     // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
-    // sharded always), so the plan that finds a solve done runs one launch later
+    // sharded always); the pass a plan finishes marks the solve done in its tail
     int late_plan() const { return (ring && (world > 1 || !split_plan)) ? 1 : 0; }
 
     int alloc(size_t bytes, void** p) {
@@ -2490,8 +2502,7 @@ static int solve_s2(SpecImpl* P, double rtol, int maxiter, int predicted, int* i
     // solve's pass count + 2, then chunks of 2.
     int passes = 0;
     (void)predicted;
-    // (+1 with the ring's late planning: the plan that finds the solve done runs one launch later)
-    const int first = P->last_passes > 0 ? P->last_passes + 2 + P->late_plan() : 8;
+    const int first = P->last_passes > 0 ? P->last_passes + 2 : 8;
     while (true) {
         const int chunk = (passes == 0) ? first : 2;
         for (int j = 0; j < chunk; ++j, ++passes) {
@@ -2592,7 +2603,7 @@ int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter,
     // FOTO_CG_MARGIN overrides the default 2 (tests force the redo path with a negative one)
     const char* me = getenv("FOTO_CG_MARGIN");
     const int margin = me ? atoi(me) : 2;
-    const int n = std::max(1, P->last_passes + margin + P->late_plan());
+    const int n = std::max(1, P->last_passes + margin);
     for (int j = 0; j < n; ++j) {
         hipEvent_t ep = kt ? kt->start(s) : nullptr;
         FOTO_HIP_CHECK(launch_s2(P, false, rtol, maxiter, nullptr, s));
@@ -2742,8 +2753,6 @@ int SpectralPlan::cg_plan(int init, double rtol, int maxiter, hipStream_t s) {
     FOTO_HIP_CHECK(hipGetLastError());
     return 0;
 }
-
-int SpectralPlan::late_extra() const { return ((const SpecImpl*)impl)->late_plan(); }
 
 int SpectralPlan::poll(int* done, int* iters, int* passes, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
