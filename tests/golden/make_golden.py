@@ -21,6 +21,13 @@ Cases (SURVEY.md §8(c) "Golden vectors to generate"):
   gn.npz         GLLOpticalFlow assemble A@x, b, process() u, v, m on 40x30 and 17x13
   io.npz         saveFlo bytes, openFlo round trip, EE/AE/IE, apply_opticalflow
   cli.npz        main.py's pipeline on a 36x28 PNG pair (FOTO Nt=4, 8 its; GN): flows, IE, .flo bytes
+  bb_metric.npz  the bench grid 640x480x32 (SURVEY.md §8(d) S-metric), run.sh params, max_it=2
+                 (~5 min): crit lines, CG counts, strided subsamples of phi after each
+                 outer iteration and of the final u, v, m
+  bb_c2s.npz     a Dimetrodon-shaped small grid 146x194x4 whose DCT half-lengths carry the
+                 prime factors 73 and 97 of the C2 grid 584x388 (textured pair, 10 its;
+                 phi, u, v, m every 5th value)
+  gn_c3.npz      GN at the C3 size 640x480 (sinusoid pair; SuperLU ~75 s): u, v, m subsample
   bin.npz        the dataset-prep scripts bin/normalize_image.py, create_lum_dataset.py and
                  data_diff.py run on a 48x40 PNG pair (decoded output pixels), and bash's
                  RANDOM sequence after RANDOM=12345 (run.sh:33 seeds create_lum_dataset)
@@ -209,7 +216,9 @@ def run_solve(bb, spla_mod, rho0, rhoT, Nt, Nx, Ny, **kw):
                 cg_info=np.array([c[0] for c in calls]), cg_its=np.array([c[1] for c in calls]))
 
 
-def gen_bb(bb, name, Nt, Nx, Ny, pair="gauss", **kw):
+def gen_bb(bb, name, Nt, Nx, Ny, pair="gauss", stride=0, **kw):
+    """stride > 0: keep every stride-th value of phi, u, v, m and no inputs (large grids; the
+    inputs are the deterministic synthetic pair, recorded by their sums)."""
     import scipy.sparse.linalg as spla
     if pair == "gauss":
         rho0, rhoT = translating_gaussian(Nx, Ny)
@@ -218,8 +227,48 @@ def gen_bb(bb, name, Nt, Nx, Ny, pair="gauss", **kw):
     res = run_solve(bb, spla, rho0, rhoT, Nt, Nx, Ny, **kw)
     params = np.array([kw.get("r", 1), kw.get("convergence_tol", 0.3), kw.get("reg_epsilon", 1e-3),
                        kw.get("max_it", 100)], dtype=np.float64)
-    save(name, shape=np.array([Nt, Ny, Nx]), params=params, rho0=rho0, rhoT=rhoT, **res)
+    if stride:
+        for k in ("phi", "u", "v", "m"):
+            res[k] = res[k][::stride]
+        save(name, shape=np.array([Nt, Ny, Nx]), params=params, stride=np.array(stride),
+             rho_sum=np.array([rho0.sum(), rhoT.sum()]), **res)
+    else:
+        save(name, shape=np.array([Nt, Ny, Nx]), params=params, rho0=rho0, rhoT=rhoT, **res)
     print(f"  {name}: {len(res['crit'])} outer its, cg its {res['cg_its'].tolist()}")
+
+
+# strides of the bench-grid subsamples: primes, so the samples walk every x, y and t phase
+METRIC_PHI_STRIDE = 499
+METRIC_FLOW_STRIDE = 37
+
+
+def gen_metric(bb):
+    """640x480x32, the bench workload (bench.py): 2 outer iterations."""
+    import scipy.sparse.linalg as spla
+    Nt, Nx, Ny = 32, 640, 480
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    xs = []
+    real = spla.cg
+
+    def cg_keep(A, b, **kw):
+        x, info = real(A, b, **kw)
+        xs.append(np.array(x[::METRIC_PHI_STRIDE]))
+        return x, info
+    spla_shim = type("S", (), {"cg": staticmethod(cg_keep)})
+    res = run_solve(bb, spla_shim, rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.01, reg_epsilon=1e-2,
+                    max_it=2)
+    sub = {k: res[k][::METRIC_FLOW_STRIDE] for k in ("u", "v", "m")}
+    save("bb_metric.npz", shape=np.array([Nt, Ny, Nx]), params=np.array([1.0, 0.01, 1e-2, 2.0]),
+         phi_stride=np.array(METRIC_PHI_STRIDE), flow_stride=np.array(METRIC_FLOW_STRIDE),
+         phi_its=np.stack(xs), crit=res["crit"], stdout=res["stdout"], cg_info=res["cg_info"],
+         cg_its=res["cg_its"], rho_sum=np.array([rho0.sum(), rhoT.sum()]), **sub)
+    print(f"  bb_metric.npz: crit {res['crit'].tolist()}, cg its {res['cg_its'].tolist()}")
+
+
+def gen_c2s(bb):
+    """Half-lengths 73 (Nx = 146) and 97 (Ny = 194): the prime factors of C2's 584x388."""
+    gen_bb(bb, "bb_c2s.npz", 4, 146, 194, pair="tex", stride=5, r=1, convergence_tol=0.01, reg_epsilon=1e-2,
+           max_it=10)
 
 
 def gen_gn(classical, rng):
@@ -247,6 +296,22 @@ def gen_gn(classical, rng):
         out[f"n{gi}_v"] = v
         out[f"n{gi}_m"] = m
     save("gn.npz", **out)
+
+
+def gen_gn_c3(classical):
+    """GN at the C3 (Grove2) size 640x480 on the synthetic sinusoid stand-in (SURVEY.md
+    §8(d)); SuperLU takes ~75 s.  u, v, m kept every METRIC_FLOW_STRIDE-th pixel."""
+    w, h, alpha, lam = 640, 480, 0.1, 0.2
+    f1, f2 = sinusoid_pair(w, h)
+    g = classical.GLLOpticalFlow(w, h)
+    g.setAlpha(alpha)
+    g.setLambda(lam)
+    g.assemble(f1, f2)
+    u, v, m = g.process()
+    s = METRIC_FLOW_STRIDE
+    save("gn_c3.npz", wh=np.array([w, h]), alpha_lambda=np.array([alpha, lam]), stride=np.array(s),
+         u=np.asarray(u)[::s], v=np.asarray(v)[::s], m=np.asarray(m)[::s],
+         b_norm=np.array(np.linalg.norm(g.b)))
 
 
 def gen_io(utils, rng):
@@ -351,17 +416,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--skip-c1", action="store_true")
+    ap.add_argument("--metric", action="store_true", help="also the 640x480x32 bench grid (~5 min)")
     ap.add_argument("--only", help="comma-separated generators to run (e.g. bin)")
     args = ap.parse_args()
-    if args.only:
-        for name in args.only.split(","):
-            {"bin": lambda: gen_bin(args.ref)}[name]()
-        return
     sys.path.insert(0, args.ref)
     import operators  # noqa: F401  (reference modules)
     import utils
     import benamou_brenier as bb
     import classical
+    if args.only:
+        for name in args.only.split(","):
+            {"bin": lambda: gen_bin(args.ref),
+             "metric": lambda: gen_metric(bb),
+             "c2s": lambda: gen_c2s(bb),
+             "gn_c3": lambda: gen_gn_c3(classical)}[name]()
+        return
 
     rng = np.random.default_rng(0)
     gen_ops(operators, rng)
@@ -375,8 +444,12 @@ def main():
     gen_bb(bb, "bb_small.npz", 4, 20, 16, r=1, convergence_tol=0.01, reg_epsilon=1e-2, max_it=30)
     gen_bb(bb, "bb_tex.npz", 5, 24, 18, pair="tex", r=1.5, convergence_tol=0.05, reg_epsilon=1e-3, max_it=12)
     gen_bin(args.ref)
+    gen_c2s(bb)
     if not args.skip_c1:
         gen_bb(bb, "bb_c1.npz", 8, 64, 64, r=1, convergence_tol=0.01, reg_epsilon=1e-2, max_it=100)
+    if args.metric:
+        gen_metric(bb)
+        gen_gn_c3(classical)
 
 
 if __name__ == "__main__":

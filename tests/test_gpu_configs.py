@@ -1,0 +1,152 @@
+"""BASELINE configs at their own sizes, against the reference (tests/golden/make_golden.py).
+
+* metric grid 640x480x32 (bench.py's workload): the reference's first two outer iterations
+  (benamou_brenier.py:204-258, scipy cg at :85) -- CG counts 147, 172, crit, phi after each
+  outer iteration and the final (u, v, m), all on strided subsamples (bb_metric.npz);
+  plus the true residual of every CG solve over ten outer iterations of the default path.
+* C2 shape: the 146x194x4 reference golden (DCT half-lengths 73 and 97, the prime factors of
+  Dimetrodon's 584x388) and the full 584x388x32 grid (mode 2 vs the literal stencil CG, true
+  residual).
+* C3: GN at 640x480 against the reference's SuperLU solve (gn_c3.npz) and its own residual.
+
+Bars (float64):
+  * CG counts +-1 (a residual norm can land within rounding of atol); crit 1e-6 relative
+    (SURVEY.md §8(c)); flow 1e-5 px (the C1 bar).
+  * phi: 1e-6 of max|phi|.  scipy's recursive residual stops at ||r|| < 1e-6 ||F||, so two
+    correct CGs whose counts differ by one differ by up to ~rtol * cond-weighted error; the
+    measured differences are printed (-s) and recorded in DESIGN.md §4.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+foto = pytest.importorskip("foto")
+from foto import ops, gn  # noqa: E402
+from foto.bb import BBSolver  # noqa: E402
+from foto.synthetic import translating_gaussian, textured_pair, sinusoid_pair  # noqa: E402
+
+RTOL_CG = 1e-6
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.abs(b).max(), 1e-300))
+
+
+def _true_residual_ok(s, mu, q, rho0, rhoT, Nt, Nx, Ny, r, eps):
+    phi = s.phi()
+    F = ops.bb_rhs(mu, q, rho0, rhoT, r, Nt, Nx, Ny)
+    res = np.linalg.norm(F - ops.apply_A(phi, Nt, Nx, Ny, r, eps))
+    return res / np.linalg.norm(F)
+
+
+@pytest.mark.parametrize("mode", [2, 0])
+def test_metric_grid_vs_reference(gold, mode):
+    d = gold("bb_metric.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    np.testing.assert_allclose([rho0.sum(), rhoT.sum()], d["rho_sum"], rtol=1e-14)
+    ps, fs = int(d["phi_stride"]), int(d["flow_stride"])
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
+        for i in range(int(max_it)):
+            s.iterate(1, tol, True)
+            e = _rel(s.phi()[::ps], d["phi_its"][i])
+            print(f"mode {mode} outer {i + 1}: cg {s.cg_its[-1]} (ref {int(d['cg_its'][i])}), "
+                  f"crit {s.crit[-1]!r} (ref {d['crit'][i]!r}), phi rel {e:.2e}")
+            assert abs(s.cg_its[-1] - int(d["cg_its"][i])) <= 1
+            assert s.cg_info[-1] == 0
+            np.testing.assert_allclose(s.crit[-1], d["crit"][i], rtol=1e-6, atol=0)
+            assert e <= 1e-6
+        u, v, m = s.flow()
+    for a, k in ((u, "u"), (v, "v"), (m, "m")):
+        err = np.abs(a[::fs] - d[k]).max()
+        print(f"mode {mode} {k}: max |d| {err:.2e} px")
+        assert err <= 1e-5
+
+
+def test_metric_grid_true_residual_ten_outer():
+    """The default path (spectral s-step CG: deferred, late-planned passes, the interval
+    adapted from the previous right-hand side) solves A phi = F to scipy's rule on every
+    outer iteration, not just the first: ||F - A phi|| <= 1.01 rtol ||F|| for ten outer
+    iterations run one call at a time, and the same crit sequence as one iterate(10) call
+    (which enqueues each next RHS before waiting: the early-head path)."""
+    Nt, Nx, Ny, r, eps = 32, 640, 480, 1.0, 1e-2
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+        for i in range(10):
+            mu, q = s.state()
+            s.iterate(1, 0.0, False)
+            rel = _true_residual_ok(s, mu, q, rho0, rhoT, Nt, Nx, Ny, r, eps)
+            print(f"outer {i + 1}: cg {s.cg_its[-1]}, true residual {rel:.3e} of ||F||")
+            assert rel <= 1.01 * RTOL_CG
+        crit_steps = np.array(s.crit)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+        s.iterate(10, 0.0, False)
+        crit_one = np.array(s.crit)
+    np.testing.assert_allclose(crit_one, crit_steps, rtol=1e-9, atol=0)
+
+
+@pytest.mark.parametrize("mode", [2, 0])
+def test_c2_shape_vs_reference(gold, mode):
+    d = gold("bb_c2s.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    st_ = int(d["stride"])
+    rho0, rhoT = textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+    np.testing.assert_allclose([rho0.sum(), rhoT.sum()], d["rho_sum"], rtol=1e-14)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
+        s.iterate(int(max_it), tol, True)
+        crit, its, phi = np.array(s.crit), np.array(s.cg_its), s.phi()
+        u, v, m = s.flow()
+    print(f"mode {mode}: cg {its.tolist()}, crit rel {_rel(crit, d['crit']):.2e}, "
+          f"phi rel {_rel(phi[::st_], d['phi']):.2e}")
+    assert len(crit) == len(d["crit"])
+    assert np.max(np.abs(its - d["cg_its"])) <= 1
+    np.testing.assert_allclose(crit, d["crit"], rtol=1e-6, atol=0)
+    assert _rel(phi[::st_], d["phi"]) <= 1e-6
+    for a, k in ((u, "u"), (v, "v"), (m, "m")):
+        err = np.abs(a[::st_] - d[k]).max()
+        print(f"mode {mode} {k}: max |d| {err:.2e} px")
+        assert err <= 1e-5
+
+
+def test_c2_full_size_spectral_vs_stencil():
+    """Dimetrodon size 584x388x32 (C2): the default spectral s-step CG against the literal
+    stencil CG for two outer iterations, and the true residual of the default path."""
+    Nt, Nx, Ny, r, eps = 32, 584, 388, 1.0, 1e-2
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = []
+    for mode in (0, 2):
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
+            rels = []
+            for _ in range(2):
+                mu, q = s.state()
+                s.iterate(1, 0.0, False)
+                rels.append(_true_residual_ok(s, mu, q, rho0, rhoT, Nt, Nx, Ny, r, eps))
+            out.append((np.array(s.cg_its), np.array(s.crit), s.phi(), rels))
+    (k0, c0, p0, r0), (k2, c2, p2, r2) = out
+    print(f"C2 cg stencil {k0.tolist()} spectral {k2.tolist()}, crit rel {_rel(c2, c0):.2e}, "
+          f"phi rel {_rel(p2, p0):.2e}, residuals {r0} {r2}")
+    assert max(r0 + r2) <= 1.01 * RTOL_CG
+    assert np.max(np.abs(k0 - k2)) <= 1
+    np.testing.assert_allclose(c2, c0, rtol=1e-6)
+    assert _rel(p2, p0) <= 1e-6
+
+
+def test_gn_c3_vs_reference(gold):
+    d = gold("gn_c3.npz")
+    w, h = (int(v) for v in d["wh"])
+    alpha, lam = d["alpha_lambda"]
+    st_ = int(d["stride"])
+    f1, f2 = sinusoid_pair(w, h)
+    u, v, m, info, its = gn.solve(f1, f2, w, h, alpha, lam)
+    assert info == 0 and 0 < its < 200
+    x = np.concatenate([u, v, m])
+    b = gn.rhs(f1, f2, w, h)
+    np.testing.assert_allclose(np.linalg.norm(b), d["b_norm"], rtol=1e-13)
+    res = np.linalg.norm(b - gn.apply(f1, f2, w, h, alpha, lam, x)) / np.linalg.norm(b)
+    errs = [np.abs(a[::st_] - d[k]).max() for a, k in ((u, "u"), (v, "v"), (m, "m"))]
+    print(f"GN 640x480: {its} PCG its, relative residual {res:.2e}, max |d| u v m {errs}")
+    assert res <= 1.01e-10
+    assert max(errs) <= 1e-7
