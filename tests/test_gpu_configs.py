@@ -9,12 +9,14 @@
   residual).
 * C3: GN at 640x480 against the reference's SuperLU solve (gn_c3.npz) and its own residual.
 
-Bars (float64):
-  * CG counts +-1 (a residual norm can land within rounding of atol); crit 1e-6 relative
-    (SURVEY.md §8(c)); flow 1e-5 px (the C1 bar).
-  * phi: 1e-6 of max|phi|.  scipy's recursive residual stops at ||r|| < 1e-6 ||F||, so two
-    correct CGs whose counts differ by one differ by up to ~rtol * cond-weighted error; the
-    measured differences are printed (-s) and recorded in DESIGN.md §4.
+Bars (float64), set ~30x above what the MI355X measured (printed with -s):
+  * CG counts +-1 (a residual norm can land within rounding of atol);
+  * bench grid: crit 1e-8 relative, phi 1e-8 of max|phi|, flow 1e-7 px (measured, default
+    s-step CG: 2.6e-10 / 3.2e-10 / 3.1e-9; stencil CG: 4e-14 / 1e-13 / 4.6e-13);
+  * C2-shaped golden: crit 1e-8, phi 1e-8, flow 1e-8 px (measured <= 2.6e-10 / 1.4e-10);
+  * C2 full size, spectral vs stencil: crit 1e-8, phi 1e-8 (measured 3.3e-10 / 1.3e-10);
+  * true residuals <= 1.01 rtol ||F|| (scipy's rule is on the recursive residual);
+  * GN 640x480 vs SuperLU: 1e-8 (measured 8.2e-10), relative residual <= 1.01e-10.
 """
 import numpy as np
 import pytest
@@ -56,13 +58,13 @@ def test_metric_grid_vs_reference(gold, mode):
                   f"crit {s.crit[-1]!r} (ref {d['crit'][i]!r}), phi rel {e:.2e}")
             assert abs(s.cg_its[-1] - int(d["cg_its"][i])) <= 1
             assert s.cg_info[-1] == 0
-            np.testing.assert_allclose(s.crit[-1], d["crit"][i], rtol=1e-6, atol=0)
-            assert e <= 1e-6
+            np.testing.assert_allclose(s.crit[-1], d["crit"][i], rtol=1e-8, atol=0)
+            assert e <= 1e-8
         u, v, m = s.flow()
     for a, k in ((u, "u"), (v, "v"), (m, "m")):
         err = np.abs(a[::fs] - d[k]).max()
         print(f"mode {mode} {k}: max |d| {err:.2e} px")
-        assert err <= 1e-5
+        assert err <= 1e-7
 
 
 def test_metric_grid_true_residual_ten_outer():
@@ -103,12 +105,12 @@ def test_c2_shape_vs_reference(gold, mode):
           f"phi rel {_rel(phi[::st_], d['phi']):.2e}")
     assert len(crit) == len(d["crit"])
     assert np.max(np.abs(its - d["cg_its"])) <= 1
-    np.testing.assert_allclose(crit, d["crit"], rtol=1e-6, atol=0)
-    assert _rel(phi[::st_], d["phi"]) <= 1e-6
+    np.testing.assert_allclose(crit, d["crit"], rtol=1e-8, atol=0)
+    assert _rel(phi[::st_], d["phi"]) <= 1e-8
     for a, k in ((u, "u"), (v, "v"), (m, "m")):
         err = np.abs(a[::st_] - d[k]).max()
         print(f"mode {mode} {k}: max |d| {err:.2e} px")
-        assert err <= 1e-5
+        assert err <= 1e-8
 
 
 def test_c2_full_size_spectral_vs_stencil():
@@ -130,8 +132,8 @@ def test_c2_full_size_spectral_vs_stencil():
           f"phi rel {_rel(p2, p0):.2e}, residuals {r0} {r2}")
     assert max(r0 + r2) <= 1.01 * RTOL_CG
     assert np.max(np.abs(k0 - k2)) <= 1
-    np.testing.assert_allclose(c2, c0, rtol=1e-6)
-    assert _rel(p2, p0) <= 1e-6
+    np.testing.assert_allclose(c2, c0, rtol=1e-8)
+    assert _rel(p2, p0) <= 1e-8
 
 
 def test_gn_c3_vs_reference(gold):
@@ -149,4 +151,4 @@ def test_gn_c3_vs_reference(gold):
     errs = [np.abs(a[::st_] - d[k]).max() for a, k in ((u, "u"), (v, "v"), (m, "m"))]
     print(f"GN 640x480: {its} PCG its, relative residual {res:.2e}, max |d| u v m {errs}")
     assert res <= 1.01e-10
-    assert max(errs) <= 1e-7
+    assert max(errs) <= 1e-8
