@@ -152,7 +152,8 @@ int foto_nccl_unique_id(void* out128);
 int foto_gn_apply(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   const double* x3, double* y3);
 int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
-/* process(): spsolve replaced by block-Jacobi PCG to rtol (default 1e-10).
+/* process(): spsolve replaced by CG preconditioned by a multigrid V-cycle (block-Jacobi
+ * smoothing, FOTO_GN_MG=0: plain block-Jacobi PCG) to rtol (default 1e-10).
  * Returns 0 (converged) or maxiter (not converged), < 0 on error.                 */
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   double rtol, int maxiter, double* u, double* v, double* m, int* iterations);

@@ -1,11 +1,13 @@
 """Drop-in for the reference's ``classical.py``: the Gennert-Negahdaripour variational
 flow with a multiplicative brightness term (classical.py:25-130), solved on the GPU.
 
-``process`` replaces SuperLU's direct solve with block-Jacobi preconditioned CG in
-libfoto.so (relative residual 1e-10 by default; agrees with spsolve to ~1e-8, see
-DESIGN.md).  ``A`` and ``b`` are still available as attributes, assembled on the host on
+``process`` replaces SuperLU's direct solve with conjugate gradients preconditioned by
+a multigrid V-cycle (replayed as a hipGraph) in libfoto.so (relative residual 1e-10 by
+default; agrees with spsolve to ~1e-8).  ``A`` and ``b`` are still available as attributes, assembled on the host on
 first access, for callers that inspect the system.
 """
+import sys
+
 import numpy as np
 from scipy import sparse
 
@@ -79,5 +81,6 @@ class GLLOpticalFlow(object):
                                        self.maxiter)
         self.iterations = its
         if info > 0:
-            print(f"WARNING: GN PCG did not converge in {info} iterations.")
+            # stderr: the reference (spsolve) never prints here, so stdout stays identical
+            print(f"WARNING: GN PCG did not converge in {info} iterations.", file=sys.stderr)
         return [u, v, m]

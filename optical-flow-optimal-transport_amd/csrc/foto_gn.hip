@@ -5,9 +5,10 @@
 //   [[-a L + fx^2, fx fy, -fx f2], [fy fx, -a L + fy^2, -fy f2], [-f2 fx, -f2 fy, -l L + f2^2]]
 // (L = 5-point Neumann Laplacian = -G^T G with G = grad_forward) and solves it with SuperLU.
 // Here the operator is applied matrix-free (one thread per pixel, all three fields) and
-// solved with block-Jacobi preconditioned CG (the per-pixel 3x3 block D + v v^T,
-// v = (fx, fy, -f2), inverted in registers by Sherman-Morrison), driven on the device
-// with the same last-block reductions as the BB CG.
+// solved with CG preconditioned by one symmetric multigrid V-cycle (damped block-Jacobi
+// smoothing with the per-pixel 3x3 block D + v v^T, v = (fx, fy, -f2); FOTO_GN_MG=0 keeps
+// plain block-Jacobi PCG), driven on the device with the same last-block reductions as
+// the BB CG and replayed as a hipGraph.
 #include "foto_internal.h"
 
 #include <algorithm>

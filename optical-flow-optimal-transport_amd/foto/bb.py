@@ -14,19 +14,22 @@ from ._lib import check, dptr, f64, lib
 
 CG_STENCIL = 0
 CG_SPECTRAL = 1
+CG_SSTEP = 2
 
 
 class BBSolver:
     """Device-resident Benamou-Brenier state (mu, q, phi stay in HBM between calls).
 
     Parameters mirror ``benamou_brenier.solve``; ``cg_mode`` picks the Poisson CG
-    (0 = 7-point stencil CG, 1 = the same CG run in the DCT-II eigenbasis of A);
+    (0 = the literal 7-point stencil CG, 1 = the same CG run in the DCT-II eigenbasis of A,
+    2 = that spectral CG in s-step passes of up to 8 iterations -- the default, as in the C
+    ABI's foto_bb_opts_default and the drop-in benamou_brenier.solve);
     ``rank/world/nccl_id`` shard the time axis over processes (RCCL),
     ``virtual_ranks`` shards it in-process on one device (test path).
     """
 
     def __init__(self, rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-3, *, device=-1, cg_rtol=1e-6,
-                 cg_maxiter=1000, cg_mode=CG_STENCIL, rank=0, world=1, nccl_id=None, virtual_ranks=1,
+                 cg_maxiter=1000, cg_mode=CG_SSTEP, rank=0, world=1, nccl_id=None, virtual_ranks=1,
                  timing=False):
         Nt, Nx, Ny = int(Nt), int(Nx), int(Ny)
         if Nt < 2:

@@ -13,7 +13,7 @@ Tolerances (float64 everywhere):
     but the oracle with a matrix-free matvec (last-bit different A p) shifts 4 of the 46
     CG counts by one and crit by 2.6e-6 relative (tests/test_oracle_golden.py::
     test_reference_rounding_sensitivity).  cg_mode 0 = stencil CG, 1 = spectral CG
-    (Chronopoulos-Gear), 2 = spectral s-step CG (s = 2).
+    (Chronopoulos-Gear), 2 = spectral s-step CG (up to 8 steps per pass).
 """
 import numpy as np
 import pytest
