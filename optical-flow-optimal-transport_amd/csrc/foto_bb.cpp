@@ -46,6 +46,7 @@ struct Shard {
     // fields: halo-padded planes (l = -1 .. nloc), pointers at local plane 0
     double* mu[3] = {nullptr, nullptr, nullptr};
     double* q[3] = {nullptr, nullptr, nullptr};
+    double* nu[3] = {nullptr, nullptr, nullptr};   // second mu buffer of the fused prox + RHS
     double* phi = nullptr;   // CG iterate x
     double* rv = nullptr;    // CG residual (starts as F)
     double* p[2] = {nullptr, nullptr};
@@ -116,6 +117,12 @@ struct foto_bb_ctx {
     int enq_its = 0, enq_info = 0;
     SpectralPlan* enq_dsp = nullptr;
     int have_phi = 0;
+    // single shard: prox fused with the next RHS (k_prox_rhs); F in rv is then produced by
+    // the previous outer iteration (f_ready), mu ping-pongs between Shard::mu and Shard::nu
+    bool fuse = false;
+    bool f_ready = false;
+    double* fz_src[3] = {nullptr, nullptr, nullptr};   // the last fused launch's mu in / out
+    double* fz_dst[3] = {nullptr, nullptr, nullptr};
     // bookkeeping
     double prev_crit = -1;
     foto_bb_stats st{};
@@ -207,6 +214,10 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_NCCL_CHECK(ncclCommInitRank(&c->nc, W, id, c->o.rank));
     }
     const int nlocal = c->rccl ? 1 : W;
+    {
+        const char* e = getenv("FOTO_FUSE_PR");   // 0: separate k_prox / k_rhs (A/B runs)
+        c->fuse = (W == 1) && !(e && atoi(e) == 0);
+    }
     for (int j = 0; j < nlocal; ++j) {
         auto sp = std::make_unique<Shard>();
         Shard& s = *sp;
@@ -217,6 +228,8 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
             return FOTO_ERR_ARG;
         }
         for (int f = 0; f < 3; ++f) { FOTO_TRY(s.alloc_field(&s.mu[f], c->s)); FOTO_TRY(s.alloc_field(&s.q[f], c->s)); }
+        if (c->fuse)
+            for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.nu[f], c->s));
         FOTO_TRY(s.alloc_field(&s.phi, c->s));
         FOTO_TRY(s.alloc_field(&s.rv, c->s));
         FOTO_TRY(s.alloc_field(&s.p[0], c->s));
@@ -230,7 +243,7 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.fv = (double*)b;
         FOTO_TRY(s.alloc(nxy * sizeof(double), &b)); s.fm = (double*)b;
         const int64_t nb = std::max<int64_t>(march_blocks(s.g), flat_blocks((int64_t)s.g.nloc * nxy));
-        s.rb.cap = (int)(2 * nb);
+        s.rb.cap = (int)std::max<int64_t>(2 * nb, 3 * (int64_t)prox_rhs_blocks(s.g));
         FOTO_TRY(s.alloc(sizeof(double) * s.rb.cap, &b)); s.rb.partials = (double*)b;
         FOTO_TRY(s.alloc(sizeof(unsigned) * 64, &b)); s.rb.ticket = (unsigned*)b;
         FOTO_HIP_CHECK(hipMemsetAsync(s.rb.ticket, 0, sizeof(unsigned) * 64, c->s));
@@ -441,6 +454,7 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 static int outer_head(foto_bb_ctx* c) {
     c->hpar ^= 1;
     FOTO_HIP_CHECK(hipEventRecord(c->phr[c->hpar], c->s));
+    if (c->fuse && c->f_ready) return 0;   // the previous iteration's k_prox_rhs wrote F (and F.F)
     FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
     FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
     for (auto& sp : c->sh) {
@@ -452,6 +466,18 @@ static int outer_head(foto_bb_ctx* c) {
         c->kt.stop(e, c->s, FOTO_K_RHS, 56.0 * nv);
     }
     if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
+    return 0;
+}
+
+// the fused k_prox_rhs on the pair recorded in fz_src -> fz_dst (single shard)
+static int prox_rhs(foto_bb_ctx* c, const int* guard) {
+    Shard& s = *c->sh[0];
+    const double nv = (double)s.g.nloc * (double)s.g.nxy;
+    hipEvent_t e = c->kt.start(c->s);
+    FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], c->fz_dst[0], c->fz_dst[1],
+                                   c->fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(1),
+                                   c->o.cg_mode == 0 ? s.gath_rr() : nullptr, c->s, guard));
+    c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
     return 0;
 }
 
@@ -482,14 +508,23 @@ static int outer_tail(foto_bb_ctx* c) {
     FOTO_HIP_CHECK(hipEventRecord(c->ph[2], c->s));
     c->have_phi = 1;
 
-    FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
-    for (auto& sp : c->sh) {
-        Shard& s = *sp;
-        const double nv = (double)s.g.nloc * (double)s.g.nxy;
-        hipEvent_t e = c->kt.start(c->s);
-        FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
-                                   s.gath_crit(W), s.rank, c->s, dsp ? dsp->done_flag() : nullptr));
-        c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+    if (c->fuse) {
+        // prox + the next iteration's RHS: mu -> nu, F -> rv; then nu is the current mu
+        Shard& s = *c->sh[0];
+        for (int f = 0; f < 3; ++f) { c->fz_src[f] = s.mu[f]; c->fz_dst[f] = s.nu[f]; }
+        FOTO_TRY(prox_rhs(c, dsp ? dsp->done_flag() : nullptr));
+        for (int f = 0; f < 3; ++f) std::swap(s.mu[f], s.nu[f]);
+        c->f_ready = true;
+    } else {
+        FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+        for (auto& sp : c->sh) {
+            Shard& s = *sp;
+            const double nv = (double)s.g.nloc * (double)s.g.nxy;
+            hipEvent_t e = c->kt.start(c->s);
+            FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
+                                       s.gath_crit(W), s.rank, c->s, dsp ? dsp->done_flag() : nullptr));
+            c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+        }
     }
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
     FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
@@ -513,10 +548,14 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             Shard& s = *c->sh[0];
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
             c->kt.discard_last(FOTO_K_PROX, 1);
-            hipEvent_t e = c->kt.start(c->s);
-            FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
-                                       s.gath_crit(W), s.rank, c->s));
-            c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+            if (c->fuse) {
+                FOTO_TRY(prox_rhs(c, nullptr));
+            } else {
+                hipEvent_t e = c->kt.start(c->s);
+                FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r,
+                                           s.rb, s.gath_crit(W), s.rank, c->s));
+                c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+            }
             FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
             FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
             FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
@@ -753,6 +792,11 @@ int foto_bb_get_phi(foto_bb_ctx* c, double* phi) {
 
 int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3) {
     if (!c) return FOTO_ERR_ARG;
+    if (q3 && c->fuse && c->have_phi) {   // the fused kernel never stores q: recompute it (bit-identical)
+        Shard& s = *c->sh[0];
+        FOTO_HIP_CHECK(launch_q_from_phi(s.g, s.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], s.q[0], s.q[1],
+                                         s.q[2], c->r, c->s));
+    }
     size_t tot = 0;
     for (auto& sp : c->sh) tot += (size_t)sp->g.nloc * sp->g.nxy;
     for (int f = 0; f < 3; ++f) {

@@ -188,6 +188,16 @@ hipError_t launch_cg_upd(const Geo& g, int k, const double* p, double* x, double
 hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
                        double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s,
                        const int* guard = nullptr);
+// single shard: k_prox fused with the next iteration's RHS (mu -> nu, F, crit num/den ->
+// gath_crit[0..1], F.F -> gath_rr[0] when non-null); needs rb.cap >= 3 * prox_rhs_blocks(g)
+int prox_rhs_blocks(const Geo& g);
+hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
+                           double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
+                           double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s,
+                           const int* guard = nullptr);
+// q = Proj_K(grad_st phi + mu / r) only (the stepB output the fused kernel does not store)
+hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut, const double* mux,
+                             const double* muy, double* qt, double* qx, double* qy, double r, hipStream_t s);
 // trajectory steps n in [n_lo, n_hi) using phi planes (local plane index l = n - t0)
 hipError_t launch_traj(const Geo& g, const double* phi, int n_lo, int n_hi, double* px, double* py,
                        int init, hipStream_t s);

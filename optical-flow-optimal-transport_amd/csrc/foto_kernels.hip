@@ -633,6 +633,258 @@ hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux
     return hipGetLastError();
 }
 
+// q = Proj_K(grad_st phi + mu / r) alone (k_prox's formulas; mu untouched): the stepB output of
+// the last outer iteration, recomputed on demand where the fused kernel below never stores it.
+__global__ __launch_bounds__(NT) void k_q_from_phi(Geo g, const double* __restrict__ phi,
+                                                   const double* __restrict__ mut, const double* __restrict__ mux,
+                                                   const double* __restrict__ muy, double* __restrict__ qt,
+                                                   double* __restrict__ qx, double* __restrict__ qy, double inv_r) {
+    const int64_t nxy = g.nxy;
+    march(g, blockIdx.x, [&](int l, int64_t off) { return phi[l * nxy + off]; },
+          [&](int l, int t, int64_t off, int x, int y, double c, double xm, double xp, double ym, double yp,
+              double tm, double tp) {
+              const int64_t i = l * nxy + off;
+              double a, b1, b2;
+              project_K(d1w(t, g.Nt, tm, c, tp) + inv_r * mut[i], d1w(x, g.Nx, xm, c, xp) + inv_r * mux[i],
+                        d1w(y, g.Ny, ym, c, yp) + inv_r * muy[i], a, b1, b2);
+              qt[i] = a;
+              qx[i] = b1;
+              qy[i] = b2;
+          });
+}
+
+hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut, const double* mux,
+                             const double* muy, double* qt, double* qx, double* qy, double r, hipStream_t s) {
+    k_q_from_phi<<<march_blocks(g), NT, 0, s>>>(g, phi, mut, mux, muy, qt, qx, qy, 1.0 / r);
+    return hipGetLastError();
+}
+
+// ============================================================================ prox + next RHS (fused)
+//
+// One outer iteration's stepB / stepC / criterion (k_prox) fused with the NEXT iteration's
+// right-hand side (k_rhs): F = div_st(mu' - r q) + BC needs only the new mu' and q of a voxel
+// and its six neighbours, so the kernel that produces them can finish F itself -- q is never
+// stored and mu' is never re-read (k_prox + k_rhs move 80 + 56 B per voxel, this kernel
+// 8 (phi) + 24 (mu) + 24 (mu') + 8 (F) = 64 B).  The price is the neighbours' stepB: a block
+// owns a 64 x 8 tile of F over a chunk of planes [l0, l1) and computes stepB on the tile plus
+// a one-voxel ring (66 x 10: the x / y neighbours F needs) and on the planes l0 - 1 and l1
+// (the t neighbours), which needs phi on a two-voxel ring (68 x 12) and planes l0 - 2 .. l1 + 1.
+// mu' goes to a second buffer (neighbouring blocks still read the old mu of their ring voxels).
+// Single shard only (the sharded path exchanges halo planes between the two halves).
+// Per voxel the arithmetic is k_prox's and k_rhs's, in the same order: mu', F and the crit
+// terms are bit-identical to the unfused kernels; only the crit / F.F sums are grouped
+// differently.
+//
+// Iteration p of the march (p = max(l0 - 1, 0) .. l1): store phi(p + 2) (loaded during the
+// previous iteration) into a 4-plane LDS ring, issue the loads of phi(p + 3) and mu(p + 1),
+// stepB on plane p (phi planes p - 1 .. p + 1 from the ring) -> w = mu' - r q of plane p into
+// a double-buffered LDS image (x, y parts; the own voxel's t part stays in registers), then
+// F(p - 1) from w of planes p - 2 .. p; one barrier per iteration.  Threads 0..147 (waves
+// 0-2) also take the 148 ring voxels.  Chunks of FOTO_PR_TCH planes (default 16) give the
+// grid more blocks than resident slots (a full-length march leaves a one-sixth-full second
+// round at 640 x 480).
+constexpr int PR_X = 64, PR_Y = 8, PR_NT = PR_X * PR_Y;   // 512 threads
+constexpr int PR_PW = PR_X + 2, PR_PH = PR_Y + 2;         // stepB region
+constexpr int PR_FW = PR_X + 4, PR_FH = PR_Y + 4;         // phi region
+constexpr int PR_HALO = 2 * PR_PW + 2 * PR_Y;             // 148 ring voxels
+constexpr int PR_FN = PR_FW * PR_FH;                      // 816 phi values per plane
+constexpr int PR_FR = (PR_FN + PR_NT - 1) / PR_NT;        // phi loads per thread per plane
+static_assert(PR_X == 64 && PR_Y == 8, "prox_rhs_blocks (foto_internal.h) assumes 64 x 8 tiles");
+
+__global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_prox_rhs(
+        Geo g, const double* __restrict__ phi, const double* __restrict__ mut, const double* __restrict__ mux,
+        const double* __restrict__ muy, double* __restrict__ nut, double* __restrict__ nux, double* __restrict__ nuy,
+        const double* __restrict__ rho0, const double* __restrict__ rhoT, double r, double inv_r,
+        double* __restrict__ F, RedBuf rb, double* gath_crit, double* gath_rr, const int* __restrict__ guard, int tch) {
+    if (guard && *guard == 0) return;
+    __shared__ double fr[4][PR_FN];                  // phi ring (plane p in slot p & 3)
+    __shared__ double wb[2][2][PR_PH * PR_PW];       // [plane & 1][x | y part] of w
+    const int Nt = g.Nt, Nx = g.Nx, Ny = g.Ny;
+    const int64_t nxy = g.nxy;
+    const int ntx = (Nx + PR_X - 1) / PR_X, ntiles = ntx * ((Ny + PR_Y - 1) / PR_Y);
+    const int lin = xcd_tile(blockIdx.x);
+    const int ch = lin / ntiles, tile = lin - ch * ntiles;
+    const int l0 = ch * tch, l1 = min(Nt, l0 + tch);
+    const int x0 = (tile % ntx) * PR_X, y0 = (tile / ntx) * PR_Y;
+    const int tid = threadIdx.x;
+    // own voxel: stepB region position (1 + tid % 64, 1 + tid / 64)
+    const int opx = 1 + (tid & (PR_X - 1)), opy = 1 + tid / PR_X;
+    const int ox = x0 - 1 + opx, oy = y0 - 1 + opy;
+    const bool own = ox < Nx && oy < Ny;
+    const int ooff = own ? oy * Nx + ox : 0;   // in-plane offsets fit 32 bits
+    // ring voxel of threads 0..147
+    int hpx = 0, hpy = 0;
+    if (tid < PR_PW) { hpx = tid; hpy = 0; }
+    else if (tid < 2 * PR_PW) { hpx = tid - PR_PW; hpy = PR_PH - 1; }
+    else if (tid < 2 * PR_PW + PR_Y) { hpx = 0; hpy = 1 + tid - 2 * PR_PW; }
+    else { hpx = PR_PW - 1; hpy = 1 + tid - 2 * PR_PW - PR_Y; }
+    const int hx = x0 - 1 + hpx, hy = y0 - 1 + hpy;
+    const bool hal = tid < PR_HALO && hx >= 0 && hx < Nx && hy >= 0 && hy < Ny;
+    const int hoff = hal ? hy * Nx + hx : 0;
+    // phi region loads of this thread
+    int foff[PR_FR];
+    bool fin[PR_FR];
+#pragma unroll
+    for (int j = 0; j < PR_FR; ++j) {
+        const int idx = tid + j * PR_NT;
+        const int fy = idx / PR_FW, fx = idx - fy * PR_FW;
+        const int xx = x0 - 2 + fx, yy = y0 - 2 + fy;
+        fin[j] = idx < PR_FN && xx >= 0 && xx < Nx && yy >= 0 && yy < Ny;
+        foff[j] = fin[j] ? yy * Nx + xx : 0;
+    }
+    const int pa = max(l0 - 1, 0), pz = min(l1, Nt - 1);   // stepB planes
+    double fv[PR_FR];
+    auto load_phi_to = [&](int p, double (&v)[PR_FR]) {   // planes beyond pz + 1 are never read
+#pragma unroll
+        for (int j = 0; j < PR_FR; ++j)
+            v[j] = (p >= 0 && p <= pz + 1 && p < Nt && fin[j]) ? phi[p * nxy + foff[j]] : 0.0;
+    };
+    auto store_phi_from = [&](int p, const double (&v)[PR_FR]) {
+#pragma unroll
+        for (int j = 0; j < PR_FR; ++j)
+            if (tid + j * PR_NT < PR_FN) fr[p & 3][tid + j * PR_NT] = v[j];
+    };
+    auto load_phi = [&](int p) { load_phi_to(p, fv); };
+    auto store_phi = [&](int p) { store_phi_from(p, fv); };
+    // mu of the own and the ring voxel, one plane ahead
+    double om[3] = {0.0, 0.0, 0.0}, hm[3] = {0.0, 0.0, 0.0};
+    auto load_mu = [&](int p) {
+        if (p > pz) return;
+        if (own) { om[0] = mut[p * nxy + ooff]; om[1] = mux[p * nxy + ooff]; om[2] = muy[p * nxy + ooff]; }
+        if (hal) { hm[0] = mut[p * nxy + hoff]; hm[1] = mux[p * nxy + hoff]; hm[2] = muy[p * nxy + hoff]; }
+    };
+    // stepB / stepC at stepB-region position (px, py) of plane t (k_prox's body)
+    auto stepb = [&](int t, int px, int py, int xg, int yg, const double (&m)[3], double (&w)[3], double& n0o,
+                     double& ao, double& gto, double& gxo, double& gyo, double (&nu)[3]) {
+        const int fi = (py + 1) * PR_FW + px + 1;
+        const double* P = fr[t & 3];
+        const double c = P[fi];
+        const double tm = t > 0 ? fr[(t - 1) & 3][fi] : 0.0, tp = t < Nt - 1 ? fr[(t + 1) & 3][fi] : 0.0;
+        const double gt = d1w(t, Nt, tm, c, tp);
+        const double gx = d1w(xg, Nx, P[fi - 1], c, P[fi + 1]);
+        const double gy = d1w(yg, Ny, P[fi - PR_FW], c, P[fi + PR_FW]);
+        double a, b1, b2;
+        project_K(gt + inv_r * m[0], gx + inv_r * m[1], gy + inv_r * m[2], a, b1, b2);
+        double n0 = m[0] + r * (gt - a);
+        n0 = (n0 < 0.0) ? 0.0 : n0;   // np.maximum(mu, 0) (NaN propagates)
+        nu[0] = n0;
+        nu[1] = m[1] + r * (gx - b1);
+        nu[2] = m[2] + r * (gy - b2);
+        w[0] = nu[0] - r * a;   // k_rhs: mu_t - r q_t, from the stored mu', q
+        w[1] = nu[1] - r * b1;
+        w[2] = nu[2] - r * b2;
+        n0o = n0;
+        ao = a;
+        gto = gt;
+        gxo = gx;
+        gyo = gy;
+    };
+    double num = 0.0, den = 0.0, ff = 0.0;
+    // own voxel: w_t of planes p-2, p-1, p; (mu'_t, q_t) of plane p-1 (bcm, bcq) and p (_n)
+    double wtm = 0.0, wtc = 0.0, wtn = 0.0, bcm = 0.0, bcq = 0.0, bcm_n = 0.0, bcq_n = 0.0;
+    // plane p's stepB for the own and the ring voxel: mu' out (own planes only), w into
+    // wb[p & 1], crit terms (own planes only)
+    auto plane = [&](int p, const double (&mo)[3], const double (&mh)[3]) {
+        const bool mine = p >= l0 && p < l1;
+        if (own) {
+            double w[3], nu[3], n0, a, gt, gx, gy;
+            stepb(p, opx, opy, ox, oy, mo, w, n0, a, gt, gx, gy, nu);
+            if (mine) {
+                const int64_t i = p * nxy + ooff;
+                nut[i] = nu[0];
+                nux[i] = nu[1];
+                nuy[i] = nu[2];
+                const double gg = gx * gx + gy * gy;
+                num += n0 * fabs(gt + 0.5 * gg);
+                den += n0 * gg;
+            }
+            wb[p & 1][0][opy * PR_PW + opx] = w[1];
+            wb[p & 1][1][opy * PR_PW + opx] = w[2];
+            wtn = w[0];
+            bcm_n = n0;
+            bcq_n = a;
+        }
+        if (hal) {
+            double w[3], nu[3], n0, a, gt, gx, gy;
+            stepb(p, hpx, hpy, hx, hy, mh, w, n0, a, gt, gx, gy, nu);
+            wb[p & 1][0][hpy * PR_PW + hpx] = w[1];
+            wb[p & 1][1][hpy * PR_PW + hpx] = w[2];
+        }
+    };
+    // prologue: phi planes pa-1 .. pa+1 in the ring, phi(pa+2) and mu(pa) in flight
+    {   // every prologue load in flight before the first LDS store
+        double f0[PR_FR], f1[PR_FR], f2[PR_FR];
+        load_phi_to(pa - 1, f0);
+        load_phi_to(pa, f1);
+        load_phi_to(pa + 1, f2);
+        load_phi(pa + 2);
+        load_mu(pa);
+        store_phi_from(pa - 1, f0);   // (pa = 0: plane -1 is never read)
+        store_phi_from(pa, f1);
+        store_phi_from(pa + 1, f2);
+    }
+    __syncthreads();
+    for (int p = pa; p <= l1; ++p) {
+        store_phi(p + 2);   // slot (p+2) & 3 = (p-2) & 3: last read by iteration p-1
+        load_phi(p + 3);
+        const double cm[3] = {om[0], om[1], om[2]}, chm[3] = {hm[0], hm[1], hm[2]};   // mu(p)
+        load_mu(p + 1);
+        if (p <= pz) plane(p, cm, chm);
+        else wtn = 0.0;   // p = Nt: F(Nt - 1) reads no w_t(Nt)
+        const int n = p - 1;
+        if (own && n >= l0) {
+            // F(n) (k_rhs's order: t, x, y terms, then the boundary-plane corrections)
+            const double* WX = wb[n & 1][0];
+            const double* WY = wb[n & 1][1];
+            const int ci = opy * PR_PW + opx;
+            double s = 0.0;
+            acc_d1w(s, n, Nt, wtm, wtc, wtn);
+            acc_d1w(s, ox, Nx, ox > 0 ? WX[ci - 1] : 0.0, WX[ci], ox < Nx - 1 ? WX[ci + 1] : 0.0);
+            acc_d1w(s, oy, Ny, oy > 0 ? WY[ci - PR_PW] : 0.0, WY[ci], oy < Ny - 1 ? WY[ci + PR_PW] : 0.0);
+            if (n == 0) s -= (rho0[ooff] - bcm) + r * bcq;
+            if (n == Nt - 1) s += (rhoT[ooff] - bcm) + r * bcq;
+            F[n * nxy + ooff] = s;
+            ff += s * s;
+        }
+        wtm = wtc;
+        wtc = wtn;
+        bcm = bcm_n;
+        bcq = bcq_n;
+        __syncthreads();
+    }
+    double v[3] = {num, den, ff}, tot[3];
+    if (grid_reduce_last<3, PR_NT>(v, rb, tot) && threadIdx.x == 0) {
+        gath_crit[0] = tot[0];
+        gath_crit[1] = tot[1];
+        if (gath_rr) gath_rr[0] = tot[2];
+    }
+}
+
+// planes per chunk (FOTO_PR_TCH, read per call for A/B tests).  Measured at 640x480x32
+// (MI355X, 2 blocks of 512 threads per CU): 4 / 8 / 16 / 32 planes -> 232 / 195 / 173 / 193 us
+// (more chunks: more recomputed boundary planes; fewer: a partly filled last round of blocks).
+int prox_rhs_tch(const Geo& g) {
+    const char* e = getenv("FOTO_PR_TCH");
+    const int v = e ? atoi(e) : 16;
+    return std::min(v > 0 ? v : 16, g.Nt);
+}
+
+int prox_rhs_blocks(const Geo& g) {
+    const int tch = prox_rhs_tch(g);
+    return ((g.Nx + PR_X - 1) / PR_X) * ((g.Ny + PR_Y - 1) / PR_Y) * ((g.Nt + tch - 1) / tch);
+}
+
+hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
+                           double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
+                           double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard) {
+    if (g.t0 != 0 || g.nloc != g.Nt) return hipErrorInvalidValue;   // single shard only
+    const int nb = prox_rhs_blocks(g);
+    if (rb.cap < 3 * nb) return hipErrorInvalidValue;
+    k_prox_rhs<<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb, gath_crit,
+                                    gath_rr, guard, prox_rhs_tch(g));
+    return hipGetLastError();
+}
+
 // ============================================================================ 2-D operators
 
 // grad_1d_central (operators.py:52-65): bc 'N' end rows zero; bc 'D' zero extension.

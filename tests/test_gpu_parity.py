@@ -278,7 +278,7 @@ def test_bb_solver_state_and_stats(gold):
     d = gold("bb_small.npz")
     Nt, Ny, Nx = (int(s) for s in d["shape"])
     r, tol, eps, _ = d["params"]
-    with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, timing=True) as s:
+    with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, timing=True, cg_mode=0) as s:
         stopped = s.iterate(3, 0.0, False)
         assert not stopped and len(s.crit) == 3
         np.testing.assert_allclose(s.crit, d["crit"][:3], rtol=1e-7)
@@ -291,6 +291,56 @@ def test_bb_solver_state_and_stats(gold):
         assert st["kernels"]["cg_dir"]["n"] >= st["cg_iters_total"]
         assert st["kernels"]["cg_upd"]["n"] >= st["cg_iters_total"]
         assert st["kernels"]["cg_dir"]["n"] <= st["cg_iters_total"] + 3 * 8
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("name", ["bb_tex.npz", "bb_c1.npz"])
+def test_bb_fused_prox_rhs_matches_separate(gold, monkeypatch, name, mode):
+    """The single-shard default fuses stepB / stepC / crit with the next iteration's RHS
+    (k_prox_rhs: F from the new mu, q of a tile plus a one-voxel ring; q never stored).  Its
+    per-voxel arithmetic is k_prox's and k_rhs's in the same order, so against the separate
+    kernels (FOTO_FUSE_PR=0) mu, phi, q (recomputed by state()) and the flow are bit-identical;
+    only the crit sums are grouped differently (1e-14).  Chunk sizes 1, 3 and the default 8
+    (planes per block) cover the chunk seams and the t = 0 / Nt - 1 boundary terms."""
+    d = gold(name)
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, _, eps, _ = d["params"]
+    res = {}
+    for key, env in (("sep", {"FOTO_FUSE_PR": "0"}), ("fused", {"FOTO_FUSE_PR": "1"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
+            s.iterate(3, 0.0, False)
+            mu, q = s.state()
+            s.iterate(2, 0.0, False)
+            res[key] = (np.array(s.crit), np.array(s.cg_its), mu, q, s.phi(), s.flow(), s.state()[0])
+    a, b = res["sep"], res["fused"]
+    assert np.array_equal(a[1], b[1])
+    if mode == 2:   # b.b comes from b^ (the DCT of F): every iterate is bit-identical
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-13, atol=0)
+        for x, y in zip(a[2:5] + a[5] + (a[6],), b[2:5] + b[5] + (b[6],)):
+            assert np.array_equal(x, y)
+    else:   # the stencil CG seeds rho_0 with F.F, summed in another order: CG rounding only
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-10, atol=0)
+        for x, y in zip(a[2:5] + a[5] + (a[6],), b[2:5] + b[5] + (b[6],)):
+            np.testing.assert_allclose(y, x, rtol=0, atol=1e-10 * max(np.abs(x).max(), 1e-300))
+
+
+@pytest.mark.parametrize("tch", ["1", "3"])
+def test_bb_fused_prox_rhs_chunks(gold, monkeypatch, tch):
+    d = gold("bb_tex.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, _, eps, _ = d["params"]
+    out = []
+    for env in ({"FOTO_FUSE_PR": "0"}, {"FOTO_FUSE_PR": "1", "FOTO_PR_TCH": tch}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+            s.iterate(3, 0.0, False)
+            out.append((s.state(), s.phi()))
+    (mu0, q0), p0 = out[0]
+    (mu1, q1), p1 = out[1]
+    assert np.array_equal(mu0, mu1) and np.array_equal(q0, q1) and np.array_equal(p0, p1)
 
 
 def test_bb_errors():
