@@ -454,7 +454,9 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 static int outer_head(foto_bb_ctx* c) {
     c->hpar ^= 1;
     FOTO_HIP_CHECK(hipEventRecord(c->phr[c->hpar], c->s));
-    if (c->fuse && c->f_ready) return 0;   // the previous iteration's k_prox_rhs wrote F (and F.F)
+    // the previous iteration's k_prox_rhs wrote F (and F.F).  (Enqueuing the next solve's x-DCT
+    // here, ahead of the crit wait, measured no faster: 457 vs 457 it/s same box.)
+    if (c->fuse && c->f_ready) return 0;
     FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
     FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
     for (auto& sp : c->sh) {
