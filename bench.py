@@ -44,6 +44,7 @@ def parse():
                     help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn", action="store_true", help="skip the GN (classical.py, config 3) side measurement")
+    ap.add_argument("--no-stencil", action="store_true", help="skip the literal stencil-CG side measurement")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--gn-cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -51,10 +52,14 @@ def parse():
     return ap.parse_args()
 
 
+CPU_K = 2   # outer iterations the CPU baseline runs (BASELINE.md / SURVEY.md §8(d): K = 2 on CPU)
+
+
 def cpu_baseline():
     """The oracle (numpy/scipy restatement, CSR SpMV + scipy-recurrence CG + vectorised
-    stepB) timed on the first outer iteration of the same workload.  Run in a child
-    process pinned to one BLAS/OpenMP thread (the reference path is single-core)."""
+    stepB) timed on the first CPU_K outer iterations of the same workload.  Run in a child
+    process pinned to one BLAS/OpenMP thread (the reference path is single-core: scipy's SpMV
+    is single-threaded, SURVEY.md §8(d) measured 8 threads no faster than 1)."""
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only"], env=env,
                          capture_output=True, text=True, timeout=900)
@@ -75,14 +80,18 @@ def cpu_baseline_child():
     mu = np.zeros(3 * N)
     for n in range(NT):
         mu[n * NX * NY:(n + 1) * NX * NY] = (1 - n / (NT - 1)) * rho0 + (n / (NT - 1)) * rhoT
+    q = np.zeros(3 * N)
+    cg = []
     t1 = time.perf_counter()
-    phi, info, its = O.solve_step(mu, np.zeros(3 * N), rho0, rhoT, R, A.dot, NT, NY, NX)
-    g = O.grad_st(phi, NT, NY, NX)
-    q = O.stepB(g + (1.0 / R) * mu, N)
-    mu = mu + R * (g - q)
-    mu[:N] = np.maximum(mu[:N], 0)
+    for _ in range(CPU_K):
+        phi, info, its = O.solve_step(mu, q, rho0, rhoT, R, A.dot, NT, NY, NX)
+        g = O.grad_st(phi, NT, NY, NX)
+        q = O.stepB(g + (1.0 / R) * mu, N)
+        mu = mu + R * (g - q)
+        mu[:N] = np.maximum(mu[:N], 0)
+        cg.append(int(its))
     loop = time.perf_counter() - t1
-    print(json.dumps({"loop_s": loop, "assemble_s": total, "cg_its": int(its)}))
+    print(json.dumps({"loop_s": loop, "assemble_s": total, "cg_its": cg, "k": CPU_K}))
 
 
 GN_W, GN_H, GN_ALPHA, GN_LAMBDA = 640, 480, 0.1, 0.2   # config 3 size, run.sh:103 parameters
@@ -100,13 +109,36 @@ def gn_cpu_child():
     print(json.dumps({"solve_s": time.perf_counter() - t}))
 
 
+def gn_levels(w, h, coarse=1024):
+    """Cell counts of the multigrid hierarchy (foto_gn.hip: halve until <= 1024 cells)."""
+    out = [(w, h)]
+    while w * h > coarse:
+        w, h = (w + 1) // 2, (h + 1) // 2
+        out.append((w, h))
+    return [a * b for a, b in out]
+
+
+def gn_bytes_per_iteration(w, h):
+    """Algorithmic HBM bytes of one MG-PCG iteration: k_gnp_dir 12 n, k_gnp_upd
+    18 n, per level k_mg_down2 18 n_l + 3 n_l+1 and k_mg_up2 21 n_l + 3 n_l+1, the coarsest
+    level 18 n_c fp64 values."""
+    ns = gn_levels(w, h)
+    v = 12 * ns[0] + 18 * ns[0]
+    for l in range(len(ns) - 1):
+        v += 18 * ns[l] + 21 * ns[l] + 6 * ns[l + 1]
+    v += 18 * ns[-1]
+    return 8 * v
+
+
 def gn_side(with_cpu):
     """GN baseline (SURVEY.md §8(d) config 3 stand-in: sinusoid pair, alpha 0.1, lambda 0.2):
-    GPU PCG solve time at 640x480 and at the CPU sample size, the oracle's spsolve beside it."""
+    GPU solve time at 640x480 and at the CPU sample size -- one-shot (foto_gn_solve: plan made,
+    used, destroyed) and with a reused plan (a batch of same-size pairs) -- and the oracle's
+    spsolve beside it."""
     from foto import gn
     from foto.synthetic import sinusoid_pair
     out = {"workload": f"GN classical solve, sinusoid pair, alpha={GN_ALPHA}, lambda={GN_LAMBDA}, "
-                       f"CG preconditioned by a symmetric multigrid V-cycle (FOTO_GN_MG=0: block-Jacobi) to rtol {gn.GN_RTOL}"}
+                       f"CG preconditioned by a symmetric multigrid V-cycle to rtol {gn.GN_RTOL}"}
     for (w, h) in ((GN_W, GN_H), (GN_CPU_W, GN_CPU_H)):
         f1, f2 = sinusoid_pair(w, h)
         best = None
@@ -115,7 +147,24 @@ def gn_side(with_cpu):
             _, _, _, info, its = gn.solve(f1, f2, w, h, GN_ALPHA, GN_LAMBDA)
             dt = time.perf_counter() - t
             best = dt if best is None else min(best, dt)
-        out[f"gpu_{w}x{h}"] = {"solve_ms": round(1e3 * best, 2), "pcg_its": its, "info": info}
+        rec = {"solve_ms": round(1e3 * best, 2), "pcg_its": its, "info": info}
+        with gn.Plan(w, h, GN_ALPHA, GN_LAMBDA) as P:
+            warm, tm = None, None
+            for _ in range(4):
+                t = time.perf_counter()
+                P.solve(f1, f2)
+                dt = time.perf_counter() - t
+                if warm is None or dt < warm:
+                    warm, tm = dt, P.timing()
+        by = gn_bytes_per_iteration(w, h)
+        ach = by * tm["iterations"] / (1e-3 * tm["ms_pcg"]) / 1e9
+        rec.update({"plan_solve_ms": round(1e3 * warm, 2), "plan_device_ms": {"setup": round(tm["ms_setup"], 3),
+                                                                               "pcg": round(tm["ms_pcg"], 3)},
+                    "us_per_pcg_it": round(1e3 * tm["ms_pcg"] / max(tm["iterations"], 1), 1),
+                    "roofline": {"bound": "hbm", "alg_bytes_per_it": by, "achieved": round(ach, 1),
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                                 "note": "PCG phase: 13 launches per iteration, small levels latency-bound"}})
+        out[f"gpu_{w}x{h}"] = rec
     if with_cpu:
         env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
         res = subprocess.run([sys.executable, os.path.abspath(__file__), "--gn-cpu-only"], env=env,
@@ -128,6 +177,32 @@ def gn_side(with_cpu):
                                              f"{GN_CPU_W}x{GN_CPU_H} pair"}
             out["speedup_vs_cpu"] = round(cpu_s / gpu_s, 1)
     return out
+
+
+def literal_stencil_rate(rho0, rhoT, device, steps=3, warmup=1):
+    """Secondary line: the literal algorithm (mode 0: scipy's CG on the 7-point stencil, no DCT
+    basis) on the same workload, so the spectral substitution is visible beside `value`."""
+    from foto.bb import BBSolver
+    with BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=device, cg_mode=0) as s:
+        s.iterate(warmup, 0.0, stop_rules=False)
+        s.sync()
+        n0 = len(s.cg_its)
+        t0 = time.perf_counter()
+        s.iterate(steps, 0.0, stop_rules=False)
+        s.sync()
+        dt = time.perf_counter() - t0
+        k = float(np.mean(s.cg_its[n0:]))
+    b = survey_bytes(k)
+    return {"cg_mode": "stencil", "value": round(steps / dt, 3), "unit": "iters/s", "steps": steps,
+            "ms_per_step": round(1e3 * dt / steps, 3), "cg_iters_per_step": round(k, 2),
+            "survey_model_gbs": round(b / (dt / steps) / 1e9, 1),
+            "survey_model_frac": round(b / (dt / steps) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def survey_bytes(k):
+    """SURVEY.md §8(d) algorithmic bytes of one outer iteration of the literal algorithm:
+    (21 + 10 k) N 8 B with k CG iterations."""
+    return (21 + 10 * k) * NX * NY * NT * 8
 
 
 def main():
@@ -243,18 +318,29 @@ def main():
             "cg_iters_per_s": round(float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,
             "phase_ms": {k: round(st_timed[k], 3) for k in ("ms_rhs", "ms_cg", "ms_prox")},
             "roofline": roof,
+            "survey_model": {"bytes_per_step": survey_bytes(float(np.mean(cg_steps))) if cg_steps else None,
+                             "equiv_gbs": round(survey_bytes(float(np.mean(cg_steps))) / (elapsed / args.steps) / 1e9, 1)
+                             if cg_steps else None,
+                             "note": "SURVEY.md 8(d) bytes of the literal stencil algorithm, (21 + 10k) N 8 B per "
+                                     "outer iteration, over this run's step time: above HBM peak because the default "
+                                     "path solves the same CG recurrence in the DCT basis (DESIGN.md 3.1)"},
             "kernels": kern,
             "epe": None,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline()
-            line["cpu_baseline"] = {"value": round(1.0 / cb["loop_s"], 6), "unit": "iters/s", "cores": 1,
-                                    "kind": "port",
+            cpu_value = cb["k"] / cb["loop_s"]
+            line["cpu_baseline"] = {"value": round(cpu_value, 6), "unit": "iters/s", "cores": 1,
+                                    "kind": "port", "nproc": os.cpu_count(),
+                                    "affinity": len(os.sched_getaffinity(0)),
                                     "sample": f"oracle (numpy/scipy CSR + scipy-rule CG + vectorised stepB), first "
-                                              f"outer iteration of the same 640x480x32 workload "
-                                              f"({cb['cg_its']} CG its, {cb['loop_s']:.1f} s loop body)"}
-            line["speedup_vs_cpu"] = round(value * cb["loop_s"], 1)
+                                              f"{cb['k']} outer iterations of the same 640x480x32 workload "
+                                              f"(CG its {cb['cg_its']}, {cb['loop_s']:.1f} s loop body), "
+                                              f"OMP/BLAS threads 1 (single-core path)"}
+            line["speedup_vs_cpu"] = round(value / cpu_value, 1)
     s.close()
+    if line is not None and world == 1 and args.cg_mode != 0 and not args.no_stencil:
+        line["literal_stencil"] = literal_stencil_rate(rho0, rhoT, local_rank)
     if line is not None and world == 1 and not args.no_gn:
         line["gn"] = gn_side(with_cpu=not args.no_cpu_baseline)
     if dist is not None:

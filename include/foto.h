@@ -154,9 +154,24 @@ int foto_gn_apply(const double* f1, const double* f2, int w, int h, double alpha
 int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
 /* process(): spsolve replaced by CG preconditioned by a multigrid V-cycle (block-Jacobi
  * smoothing, FOTO_GN_MG=0: plain block-Jacobi PCG) to rtol (default 1e-10).
- * Returns 0 (converged) or maxiter (not converged), < 0 on error.                 */
+ * Returns 0 (converged) or maxiter (not converged), < 0 on error.  One-shot: a plan is made,
+ * used once and destroyed.                                                        */
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   double rtol, int maxiter, double* u, double* v, double* m, int* iterations);
+
+/* A reusable GLLOpticalFlow(w, h) with setAlpha/setLambda applied (classical.py:25-66): device
+ * buffers, the multigrid hierarchy and the replayed PCG graph are made once; every
+ * foto_gn_plan_solve is one process(f1, f2) (classical.py:68-130: coefficients, right-hand
+ * side, multigrid coefficients, PCG) with the same result and return codes as foto_gn_solve.
+ * Batches of same-size pairs (run.sh:81-157) reuse one plan.                       */
+typedef struct foto_gn_plan foto_gn_plan;
+int foto_gn_plan_create(int w, int h, double alpha, double lambda_, double rtol, int maxiter, foto_gn_plan** out);
+int foto_gn_plan_solve(foto_gn_plan* p, const double* f1, const double* f2, double* u, double* v, double* m,
+                       int* iterations);
+/* the last solve: {ms upload + setup + V-cycle of r0, ms PCG iterations (device events),
+ * iterations, iterations launched}                                                */
+int foto_gn_plan_timing(const foto_gn_plan* p, double* out4);
+void foto_gn_plan_destroy(foto_gn_plan* p);
 
 /* ------------------------------------------------------------------ evaluation
  * the warp and the error metrics of utils.py on the GPU.      */

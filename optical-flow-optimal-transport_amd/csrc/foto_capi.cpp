@@ -284,6 +284,15 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
         return FOTO_ERR_ARG;
     }
     if (maxiter < 0) { set_error("maxiter < 0"); return FOTO_ERR_ARG; }
+    const char* emg = getenv("FOTO_GN_MG");   // 0: 3x3 block-Jacobi preconditioner (A/B runs)
+    if (!(emg && atoi(emg) == 0)) {
+        // multigrid-preconditioned CG through a one-shot plan (foto_gn.hip)
+        foto_gn_plan* P = nullptr;
+        FOTO_TRY(foto_gn_plan_create(w, h, alpha, lam, rtol, maxiter, &P));
+        std::unique_ptr<foto_gn_plan, void (*)(foto_gn_plan*)> pg(P, foto_gn_plan_destroy);
+        return foto_gn_plan_solve(P, f1, f2, u, v, m, iterations);
+    }
+    // 3x3 block-Jacobi PCG (the first GPU version; kept for A/B runs)
     Scope S;
     FOTO_TRY(S.init());
     const size_t n = (size_t)w * h;
@@ -315,55 +324,7 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
     std::unique_ptr<CGScal, void (*)(CGScal*)> hguard(hS, [](CGScal* p) { (void)hipHostFree(p); });
     int k = 0;
     bool done = false;
-    const char* emg = getenv("FOTO_GN_MG");   // 0: 3x3 block-Jacobi preconditioner (A/B runs)
-    if (!(emg && atoi(emg) == 0)) {
-        // Multigrid-preconditioned CG (foto_gn.hip): the init above already formed z with the
-        // block-Jacobi preconditioner; redo r = b, r.r and z = V(r), r.z.  Two iterations
-        // (p0 -> p1 -> p0) are captured once as a hipGraph (about 2 x (3 + 4 levels) small
-        // launches; the kernels read the iteration index from the device) and replayed.
-        GnMG mg;
-        FOTO_TRY(mg.setup(w, h, fx, fy, d2, alpha, lam, S.s));
-        FOTO_HIP_CHECK(launch_gn_mg_init((int64_t)n, b, r, rb, g_rz, S.s));
-        FOTO_TRY(mg.vcycle(r, z, dS, rb, g_rz, S.s));
-        auto iteration = [&](double* po, double* pn) -> int {
-            FOTO_HIP_CHECK(launch_gn_pcg_dir(w, h, -1, fx, fy, d2, alpha, lam, z, po, pn, dS, rb, g_rz, g_pq, rtol, S.s));
-            FOTO_HIP_CHECK(launch_gn_mg_upd(w, h, fx, fy, d2, alpha, lam, pn, x, r, dS, rb, g_pq, g_rz, S.s));
-            return mg.vcycle(r, z, dS, rb, g_rz, S.s);
-        };
-        const char* eg = getenv("FOTO_GN_GRAPH");
-        if (eg && atoi(eg) == 0) {   // direct launches (A/B runs)
-            while (k < maxiter) {
-                const int chunk = std::min(k == 0 ? 16 : 8, maxiter - k);
-                for (int j = 0; j < chunk; ++j, ++k) FOTO_TRY((k & 1) ? iteration(p1, p0) : iteration(p0, p1));
-                FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
-                FOTO_TRY(S.sync());
-                if (hS->done) { done = true; break; }
-            }
-            k = maxiter;   // skip the graph loop below
-        }
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t gexec = nullptr;
-        FOTO_HIP_CHECK(hipStreamBeginCapture(S.s, hipStreamCaptureModeThreadLocal));
-        const int c1 = iteration(p0, p1), c2 = c1 < 0 ? c1 : iteration(p1, p0);
-        const hipError_t ec = hipStreamEndCapture(S.s, &graph);
-        std::unique_ptr<void, void (*)(void*)> gg(graph, [](void* g) { if (g) (void)hipGraphDestroy((hipGraph_t)g); });
-        FOTO_TRY(c2);
-        FOTO_HIP_CHECK(ec);
-        FOTO_HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
-        std::unique_ptr<void, void (*)(void*)> ge(gexec, [](void* g) { (void)hipGraphExecDestroy((hipGraphExec_t)g); });
-        while (k < maxiter) {
-            const int chunk = std::min(k == 0 ? 16 : 8, maxiter - k);
-            int j = 0;
-            for (; j + 2 <= chunk; j += 2, k += 2) FOTO_HIP_CHECK(hipGraphLaunch(gexec, S.s));
-            if (j < chunk) {   // odd maxiter: one last iteration outside the graph (k even: p0 -> p1)
-                FOTO_TRY(iteration(p0, p1));
-                ++k;
-            }
-            FOTO_HIP_CHECK(hipMemcpyAsync(hS, dS, sizeof(CGScal), hipMemcpyDeviceToHost, S.s));
-            FOTO_TRY(S.sync());
-            if (hS->done) { done = true; break; }
-        }
-    } else {
+    {
         while (k < maxiter) {
             const int chunk = std::min(k == 0 ? 64 : 32, maxiter - k);
             for (int j = 0; j < chunk; ++j, ++k) {

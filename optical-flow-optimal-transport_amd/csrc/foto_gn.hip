@@ -12,6 +12,8 @@
 #include "foto_internal.h"
 
 #include <algorithm>
+#include <memory>
+#include <vector>
 
 namespace foto {
 
@@ -352,7 +354,8 @@ hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double
 }
 
 
-// ============================================================================ multigrid preconditioner
+
+// ============================================================================ multigrid-preconditioned CG
 //
 // PCG on the GN system (classical.py:68-130) preconditioned by one symmetric V-cycle:
 // cell-centred levels (w, h) -> (ceil(w/2), ceil(h/2)) down to at most MG_COARSE cells;
@@ -363,15 +366,25 @@ hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double
 // 3/4, 1/4 per axis, indices clamped at the Neumann boundary), restriction R = P^T / 4;
 // one damped (omega = 0.8) block-Jacobi sweep before and after the coarse correction, the
 // coarsest level smoothed MG_CSWEEPS times from zero in one block.  Every piece is a fixed
-// symmetric linear operator, so the V-cycle is a valid CG preconditioner.  Numpy prototype
-// (320x240 sinusoid pair, rtol 1e-10): 33 PCG iterations instead of ~940 with the 3x3
-// block-Jacobi preconditioner; the solve still meets SuperLU's answer to ~1e-9.
-// Any approximation here only changes the preconditioner: the PCG applies the exact operator
-// (gn_row, CSR order) and stops on the exact residual norm.
+// symmetric linear operator, so the V-cycle is a valid CG preconditioner.  Any approximation
+// here only changes the preconditioner: the PCG applies the exact operator (gn_row, CSR
+// order) and stops on the exact residual norm.
+//
+// Launch structure (13 kernels per PCG iteration at 640x480, replayed as a hipGraph):
+//   k_gnp_dir   stop test, beta, p = z + beta p, q = A p, partial p.q
+//   k_gnp_upd   alpha, x += alpha p, r -= alpha A p, partial r.r
+//   k_mg_down2  per level: pre-smoothing from zero, residual and restriction in one LDS tile
+//   k_mg_coarse the coarsest level in one block
+//   k_mg_up2    per level: prolongation of the coarse correction and post-smoothing in one
+//               LDS tile (level 0: z and the partial r.z)
+// Global sums are consumer-side: every reducing kernel stores one partial per block (no
+// atomics, no ticket), and every kernel that needs the sum adds the partials in the same
+// fixed order in each of its blocks, so all blocks take identical decisions.
 
 constexpr int MG_COARSE = 1024;   // cells of the coarsest level (one block, one cell per thread)
 constexpr int MG_CSWEEPS = 48;
 constexpr double MG_OMEGA = 0.8;
+constexpr int GT_X = 32, GT_Y = 16;   // fine tile of the level kernels (256 threads, 2 cells each)
 
 struct MGLev {
     int w, h;
@@ -380,39 +393,18 @@ struct MGLev {
     const double* Dinv;   // 6 planes: inverse of the cell's 3x3 diagonal block (symmetric)
 };
 
+static inline int mg_tiles(int w, int h) { return ((w + GT_X - 1) / GT_X) * ((h + GT_Y - 1) / GT_Y); }
+
 __device__ __forceinline__ int mg_ncount(int x, int y, int w, int h) {
     return (x > 0) + (x < w - 1) + (y > 0) + (y < h - 1);
 }
 
-// 1-D weight of coarse index I for fine index i (n fine cells, nc coarse), clamped
+// 1-D prolongation weight of coarse index I for fine index i (nc coarse cells), clamped
 __device__ __forceinline__ double mg_w1(int i, int I, int nc) {
     const int I0 = i >> 1;
     int I1 = (i & 1) ? I0 + 1 : I0 - 1;
     I1 = I1 < 0 ? 0 : (I1 > nc - 1 ? nc - 1 : I1);
     return (I0 == I ? 0.75 : 0.0) + (I1 == I ? 0.25 : 0.0);
-}
-
-// (A x)_f for cell (x, y) of level L; X(f, idx) loads the vector
-template <class F>
-__device__ __forceinline__ void mg_apply(const MGLev& L, int x, int y, int64_t i, F X, double& a0, double& a1,
-                                         double& a2) {
-    const int64_t n = (int64_t)L.w * L.h;
-    const int64_t jxm = x > 0 ? i - 1 : i, jxp = x < L.w - 1 ? i + 1 : i;
-    const int64_t jym = y > 0 ? i - L.w : i, jyp = y < L.h - 1 ? i + L.w : i;
-    const double c = (double)mg_ncount(x, y, L.w, L.h);
-    double v[3], nb[3];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-        v[f] = X(f, i);
-        const double xm = X(f, jxm), xp = X(f, jxp), ym = X(f, jym), yp = X(f, jyp);
-        nb[f] = (x > 0 ? xm : 0.0) + (x < L.w - 1 ? xp : 0.0) + (y > 0 ? ym : 0.0) + (y < L.h - 1 ? yp : 0.0);
-    }
-    const double* B = L.B;
-    const double bxx = B[i], bxy = B[n + i], bxm = B[2 * n + i], byy = B[3 * n + i], bym = B[4 * n + i],
-                 bmm = B[5 * n + i];
-    a0 = L.s0 * (c * v[0] - nb[0]) + bxx * v[0] + bxy * v[1] + bxm * v[2];
-    a1 = L.s1 * (c * v[1] - nb[1]) + bxy * v[0] + byy * v[1] + bym * v[2];
-    a2 = L.s2 * (c * v[2] - nb[2]) + bxm * v[0] + bym * v[1] + bmm * v[2];
 }
 
 __device__ __forceinline__ void mg_dinv(const MGLev& L, int64_t i, double r0, double r1, double r2, double& z0,
@@ -425,6 +417,180 @@ __device__ __forceinline__ void mg_dinv(const MGLev& L, int64_t i, double r0, do
     z1 = d01 * r0 + d11 * r1 + d12 * r2;
     z2 = d02 * r0 + d12 * r1 + d22 * r2;
 }
+
+// (A x) of cell (x, y) = global index i, with the vector in an LDS tile: X(f, dy, dx) is the
+// value at the neighbour offset (dy, dx) in {-1, 0, 1}; neighbours outside the grid are skipped
+template <class F>
+__device__ __forceinline__ void mg_apply_t(const MGLev& L, int x, int y, int64_t i, F X, double& a0, double& a1,
+                                           double& a2, double& v0, double& v1, double& v2) {
+    const int64_t n = (int64_t)L.w * L.h;
+    const bool hxm = x > 0, hxp = x < L.w - 1, hym = y > 0, hyp = y < L.h - 1;
+    const double c = (double)((int)hxm + (int)hxp + (int)hym + (int)hyp);
+    double v[3], nb[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        v[f] = X(f, 0, 0);
+        nb[f] = (hxm ? X(f, 0, -1) : 0.0) + (hxp ? X(f, 0, 1) : 0.0) + (hym ? X(f, -1, 0) : 0.0) +
+                (hyp ? X(f, 1, 0) : 0.0);
+    }
+    const double* B = L.B;
+    const double bxx = B[i], bxy = B[n + i], bxm = B[2 * n + i], byy = B[3 * n + i], bym = B[4 * n + i],
+                 bmm = B[5 * n + i];
+    a0 = L.s0 * (c * v[0] - nb[0]) + bxx * v[0] + bxy * v[1] + bxm * v[2];
+    a1 = L.s1 * (c * v[1] - nb[1]) + bxy * v[0] + byy * v[1] + bym * v[2];
+    a2 = L.s2 * (c * v[2] - nb[2]) + bxm * v[0] + bym * v[1] + bmm * v[2];
+    v0 = v[0]; v1 = v[1]; v2 = v[2];
+}
+
+// ----------------------------------------------------------------------------- consumer-side sums
+
+// sum of the nb partials of each of K arrays, in the same fixed order in every block
+// (thread t adds t, t + NT, ...; then a fixed shuffle tree and the 4 wave sums in order)
+template <int K>
+__device__ __forceinline__ void mg_sum_partials(const double* const (&src)[K], int nb, double (&out)[K]) {
+    __shared__ double sh[K][NT / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double v = 0.0;
+        for (int i = threadIdx.x; i < nb; i += NT) v += src[k][i];
+        v = gn_wave_sum(v);
+        if (lane == 0) sh[k][wv] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double s = sh[k][0];
+#pragma unroll
+        for (int j = 1; j < NT / 64; ++j) s += sh[k][j];
+        out[k] = s;
+    }
+}
+
+// this block's partial of v -> dst[block] (fixed order)
+__device__ __forceinline__ void mg_block_partial(double v, double* dst) {
+    __shared__ double sh[NT / 64];
+    v = gn_wave_sum(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = sh[0];
+#pragma unroll
+        for (int j = 1; j < NT / 64; ++j) s += sh[j];
+        dst[blockIdx.x] = s;
+    }
+}
+
+// ----------------------------------------------------------------------------- PCG kernels
+
+// r = b, partial r.r
+__global__ __launch_bounds__(NT) void k_gnp_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
+                                                 double* __restrict__ rr_part) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double rr = 0.0;
+    if (i < n) {
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const double v = b[f * n + i];
+            r[f * n + i] = v;
+            rr += v * v;
+        }
+    }
+    mg_block_partial(rr, rr_part);
+}
+
+// iteration k (S->pad[0]): stop test on ||r_k|| (atol = rtol ||b|| fixed at k = 0), beta =
+// rz_k / rz_{k-1}, p_k = z_k + beta p_{k-1} (for the pixel and its 4 neighbours), q = A p_k,
+// partial p.q; writes p_k.
+__global__ __launch_bounds__(NT) void k_gnp_dir(int w, int h, const double* __restrict__ fx,
+                                                const double* __restrict__ fy, const double* __restrict__ f2,
+                                                double a, double l, const double* __restrict__ z,
+                                                const double* __restrict__ po, double* __restrict__ pn, CGScal* S,
+                                                const double* rr_part, int nb_rr, const double* rz_cur,
+                                                const double* rz_prev, int nb_rz, double* __restrict__ pq_part,
+                                                double rtol) {
+    if (S->done) return;
+    const int k = S->pad[0];
+    double rr, rzc, rzp;
+    {
+        const double* src[2] = {rz_cur, rz_prev};
+        double o[2];
+        mg_sum_partials<2>(src, nb_rz, o);
+        rzc = o[0];
+        rzp = o[1];
+        const double* s1[1] = {rr_part};
+        double o1[1];
+        __syncthreads();   // mg_sum_partials' LDS is reused
+        mg_sum_partials<1>(s1, nb_rr, o1);
+        rr = o1[0];
+    }
+    const double atol = (k == 0) ? fmax(0.0, rtol * sqrt(rr)) : S->atol;
+    if (rr == 0.0 || sqrt(rr) < atol) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { S->done = 1; S->iters = k; }
+        return;
+    }
+    if (k == 0 && blockIdx.x == 0 && threadIdx.x == 0) { S->bb = rr; S->atol = atol; }
+    const double beta = (k > 0) ? rzc / rzp : 0.0;
+    const int64_t n = (int64_t)w * h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double pq = 0.0;
+    if (i < n) {
+        const GNPix P = gn_pix(w, h, i);
+        auto pv = [&](int f, int64_t j) -> double {
+            const int64_t o = f * n + j;
+            return (k == 0) ? z[o] : beta * po[o] + z[o];
+        };
+        double qu, qv, qm;
+        gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, pv, qu, qv, qm);
+        const double pu = pv(0, i), pvv = pv(1, i), pm = pv(2, i);
+        pn[i] = pu; pn[n + i] = pvv; pn[2 * n + i] = pm;
+        pq = pu * qu + pvv * qv + pm * qm;
+    }
+    mg_block_partial(pq, pq_part);
+}
+
+// alpha = rz_k / p.q; x += alpha p (x starts at 0); r -= alpha A p; partial r.r; k += 1
+__global__ __launch_bounds__(NT) void k_gnp_upd(int w, int h, const double* __restrict__ fx,
+                                                const double* __restrict__ fy, const double* __restrict__ f2,
+                                                double a, double l, const double* __restrict__ p,
+                                                double* __restrict__ x, double* __restrict__ r, CGScal* S,
+                                                const double* rz_cur, int nb_rz, const double* pq_part, int nb_pq,
+                                                double* __restrict__ rr_part) {
+    if (S->done) return;
+    double alpha;
+    {
+        const double* s1[1] = {rz_cur};
+        double o1[1];
+        mg_sum_partials<1>(s1, nb_rz, o1);
+        const double* s2[1] = {pq_part};
+        double o2[1];
+        __syncthreads();
+        mg_sum_partials<1>(s2, nb_pq, o2);
+        alpha = o1[0] / o2[0];
+    }
+    const int64_t n = (int64_t)w * h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double rr = 0.0;
+    if (i < n) {
+        const GNPix P = gn_pix(w, h, i);
+        double qu, qv, qm;
+        gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, [&](int f, int64_t j) { return p[f * n + j]; }, qu, qv, qm);
+        const double q3[3] = {qu, qv, qm};
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const int64_t o = f * n + i;
+            x[o] = x[o] + alpha * p[o];
+            const double rn = r[o] - alpha * q3[f];
+            r[o] = rn;
+            rr += rn * rn;
+        }
+    }
+    mg_block_partial(rr, rr_part);
+    // the iteration index: read by k_gnp_dir only, so no block of this launch races with it
+    if (blockIdx.x == 0 && threadIdx.x == 0) S->pad[0] = S->pad[0] + 1;
+}
+
+// ----------------------------------------------------------------------------- V-cycle kernels
 
 __global__ __launch_bounds__(NT) void k_mg_b0(int64_t n, const double* __restrict__ fx, const double* __restrict__ fy,
                                               const double* __restrict__ f2, double* __restrict__ B) {
@@ -447,10 +613,9 @@ __global__ __launch_bounds__(NT) void k_mg_coarsen(int w, int h, const double* _
     if (I >= nc) return;
     const int J = (int)(I / wc), K = (int)(I - (int64_t)J * wc);
     double acc[6] = {0, 0, 0, 0, 0, 0}, ws = 0.0;
-    for (int y = max(0, 2 * J - 2); y <= min(h - 1, 2 * J + 3); ++y) {
+    for (int y = max(0, 2 * J - 1); y <= min(h - 1, 2 * J + 2); ++y) {
         const double wy = mg_w1(y, J, hc);
-        if (wy == 0.0) continue;
-        for (int x = max(0, 2 * K - 2); x <= min(w - 1, 2 * K + 3); ++x) {
+        for (int x = max(0, 2 * K - 1); x <= min(w - 1, 2 * K + 2); ++x) {
             const double wgt = wy * mg_w1(x, K, wc);
             if (wgt == 0.0) continue;
             const int64_t i = (int64_t)y * w + x;
@@ -485,109 +650,138 @@ __global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Di
     Dinv[5 * n + i] = c22 * id;
 }
 
-// pre-smoothing from zero fused with the residual: x = omega D^-1 f, r = f - A x
-__global__ __launch_bounds__(NT) void k_mg_down(MGLev L, const CGScal* S, const double* __restrict__ f,
-                                                double* __restrict__ x, double* __restrict__ r) {
+// Down leg of one level, one GT_Y x GT_X fine tile per block:
+//   x = omega D^-1 f (pre-smoothing from zero) over the tile + 2 halo cells   -> LDS
+//   r = f - A x over the tile + 1 halo cell                                   -> LDS; x -> xg
+//   fc = R r = P^T r / 4 for the tile's GT_Y/2 x GT_X/2 coarse cells (4 x 4 taps) -> fc
+__global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const CGScal* S,
+                                                 const double* __restrict__ f, double* __restrict__ xg,
+                                                 double* __restrict__ fc) {
     if (S->done) return;
-    const int64_t n = (int64_t)L.w * L.h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-    if (i >= n) return;
-    const int y = (int)((unsigned)i / (unsigned)L.w), xx = (int)i - y * L.w;
-    auto X = [&](int fld, int64_t j) {
-        double z0, z1, z2;
-        mg_dinv(L, j, f[j], f[n + j], f[2 * n + j], z0, z1, z2);
-        return MG_OMEGA * (fld == 0 ? z0 : (fld == 1 ? z1 : z2));
-    };
-    double a0, a1, a2;
-    mg_apply(L, xx, y, i, X, a0, a1, a2);
-    x[i] = X(0, i);
-    x[n + i] = X(1, i);
-    x[2 * n + i] = X(2, i);
-    r[i] = f[i] - a0;
-    r[n + i] = f[n + i] - a1;
-    r[2 * n + i] = f[2 * n + i] - a2;
-}
-
-// fc = R r = P^T r / 4
-__global__ __launch_bounds__(NT) void k_mg_restrict(int w, int h, const CGScal* S, const double* __restrict__ r,
-                                                    int wc, int hc, double* __restrict__ fc) {
-    if (S->done) return;
-    const int64_t nc = (int64_t)wc * hc, n = (int64_t)w * h;
-    const int64_t I = (int64_t)blockIdx.x * NT + threadIdx.x;
-    if (I >= nc) return;
-    const int J = (int)(I / wc), K = (int)(I - (int64_t)J * wc);
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    for (int y = max(0, 2 * J - 2); y <= min(h - 1, 2 * J + 3); ++y) {
-        const double wy = mg_w1(y, J, hc);
-        if (wy == 0.0) continue;
-        for (int x = max(0, 2 * K - 2); x <= min(w - 1, 2 * K + 3); ++x) {
-            const double wgt = wy * mg_w1(x, K, wc);
-            if (wgt == 0.0) continue;
-            const int64_t i = (int64_t)y * w + x;
-            a0 += wgt * r[i];
-            a1 += wgt * r[n + i];
-            a2 += wgt * r[2 * n + i];
+    constexpr int XW = GT_X + 4, XH = GT_Y + 4, RW = GT_X + 2, RH = GT_Y + 2;
+    __shared__ double xs[3][XH][XW];
+    __shared__ double rs[3][RH][RW];
+    const int w = L.w, h = L.h;
+    const int64_t n = (int64_t)w * h;
+    const int tiles_x = (w + GT_X - 1) / GT_X;
+    const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
+    for (int c = threadIdx.x; c < XH * XW; c += NT) {
+        const int ly = c / XW, lx = c - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
+        double z0 = 0.0, z1 = 0.0, z2 = 0.0;
+        if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+            const int64_t i = (int64_t)gy * w + gx;
+            mg_dinv(L, i, f[i], f[n + i], f[2 * n + i], z0, z1, z2);
+            z0 *= MG_OMEGA; z1 *= MG_OMEGA; z2 *= MG_OMEGA;
         }
+        xs[0][ly][lx] = z0; xs[1][ly][lx] = z1; xs[2][ly][lx] = z2;
     }
-    fc[I] = 0.25 * a0;
-    fc[nc + I] = 0.25 * a1;
-    fc[2 * nc + I] = 0.25 * a2;
-}
-
-// x += P ec
-__global__ __launch_bounds__(NT) void k_mg_prolong(int w, int h, const CGScal* S, const double* __restrict__ ec,
-                                                   int wc, int hc, double* __restrict__ x) {
-    if (S->done) return;
-    const int64_t n = (int64_t)w * h, nc = (int64_t)wc * hc;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-    if (i >= n) return;
-    const int y = (int)((unsigned)i / (unsigned)w), xx = (int)i - y * w;
-    const int X0 = xx >> 1, Y0 = y >> 1;
-    int X1 = (xx & 1) ? X0 + 1 : X0 - 1, Y1 = (y & 1) ? Y0 + 1 : Y0 - 1;
-    X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
-    Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
-    const int64_t c00 = (int64_t)Y0 * wc + X0, c01 = (int64_t)Y0 * wc + X1, c10 = (int64_t)Y1 * wc + X0,
-                  c11 = (int64_t)Y1 * wc + X1;
+    __syncthreads();
+    for (int c = threadIdx.x; c < RH * RW; c += NT) {
+        const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+        if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+            const int64_t i = (int64_t)gy * w + gx;
+            double a0, a1, a2, v0, v1, v2;
+            mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0, a1,
+                       a2, v0, v1, v2);
+            r0 = f[i] - a0; r1 = f[n + i] - a1; r2 = f[2 * n + i] - a2;
+            if (ly >= 1 && ly <= GT_Y && lx >= 1 && lx <= GT_X) { xg[i] = v0; xg[n + i] = v1; xg[2 * n + i] = v2; }
+        }
+        rs[0][ly][lx] = r0; rs[1][ly][lx] = r1; rs[2][ly][lx] = r2;
+    }
+    __syncthreads();
+    const int64_t nc = (int64_t)wc * hc;
+    for (int c = threadIdx.x; c < (GT_Y / 2) * (GT_X / 2); c += NT) {
+        const int cy = c / (GT_X / 2), cx = c - cy * (GT_X / 2);
+        const int J = y0 / 2 + cy, K = x0 / 2 + cx;
+        if (J >= hc || K >= wc) continue;
+        double wy[4], wx[4];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-        const double* e = ec + f * nc;
-        x[f * n + i] += 0.5625 * e[c00] + 0.1875 * e[c01] + 0.1875 * e[c10] + 0.0625 * e[c11];
+        for (int d = 0; d < 4; ++d) {
+            const int y = 2 * J - 1 + d, x = 2 * K - 1 + d;
+            wy[d] = (y >= 0 && y < h) ? mg_w1(y, J, hc) : 0.0;
+            wx[d] = (x >= 0 && x < w) ? mg_w1(x, K, wc) : 0.0;
+        }
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) {
+            double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx) {
+                const int ly = 2 * cy + dy, lx = 2 * cx + dx;   // (2J - 1 + dy) - (y0 - 1)
+                b0 += wx[dx] * rs[0][ly][lx];
+                b1 += wx[dx] * rs[1][ly][lx];
+                b2 += wx[dx] * rs[2][ly][lx];
+            }
+            a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * b2;
+        }
+        const int64_t I = (int64_t)J * wc + K;
+        fc[I] = 0.25 * a0;
+        fc[nc + I] = 0.25 * a1;
+        fc[2 * nc + I] = 0.25 * a2;
     }
 }
 
-// xo = xi + omega D^-1 (f - A xi); RZ: partial sum of f . xo -> gath_rz[1] (the PCG's r.z)
+// Up leg of one level, one GT_Y x GT_X fine tile per block:
+//   x' = x + P ec over the tile + 1 halo cell -> LDS
+//   out = x' + omega D^-1 (f - A x') on the tile; RZ: partial f . out -> rz_part[block]
 template <bool RZ>
-__global__ __launch_bounds__(NT) void k_mg_smooth(MGLev L, const CGScal* S, const double* __restrict__ f,
-                                                  const double* __restrict__ xi, double* __restrict__ xo,
-                                                  RedBuf rb, double* gath_rz) {
+__global__ __launch_bounds__(NT) void k_mg_up2(MGLev L, int wc, int hc, const CGScal* S,
+                                               const double* __restrict__ ec, const double* __restrict__ f,
+                                               const double* __restrict__ xg, double* __restrict__ out,
+                                               double* __restrict__ rz_part) {
     if (S->done) return;
-    const int64_t n = (int64_t)L.w * L.h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    constexpr int RW = GT_X + 2, RH = GT_Y + 2;
+    __shared__ double xs[3][RH][RW];
+    const int w = L.w, h = L.h;
+    const int64_t n = (int64_t)w * h, nc = (int64_t)wc * hc;
+    const int tiles_x = (w + GT_X - 1) / GT_X;
+    const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
+    for (int c = threadIdx.x; c < RH * RW; c += NT) {
+        const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+        double v[3] = {0.0, 0.0, 0.0};
+        if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+            const int64_t i = (int64_t)gy * w + gx;
+            const int X0 = gx >> 1, Y0 = gy >> 1;
+            int X1 = (gx & 1) ? X0 + 1 : X0 - 1, Y1 = (gy & 1) ? Y0 + 1 : Y0 - 1;
+            X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
+            Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
+            const int64_t c00 = (int64_t)Y0 * wc + X0, c01 = (int64_t)Y0 * wc + X1, c10 = (int64_t)Y1 * wc + X0,
+                          c11 = (int64_t)Y1 * wc + X1;
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) {
+                const double* e = ec + fl * nc;
+                v[fl] = xg[fl * n + i] + (0.5625 * e[c00] + 0.1875 * e[c01] + 0.1875 * e[c10] + 0.0625 * e[c11]);
+            }
+        }
+        xs[0][ly][lx] = v[0]; xs[1][ly][lx] = v[1]; xs[2][ly][lx] = v[2];
+    }
+    __syncthreads();
     double rz = 0.0;
-    if (i < n) {
-        const int y = (int)((unsigned)i / (unsigned)L.w), xx = (int)i - y * L.w;
-        double a0, a1, a2, z0, z1, z2;
-        mg_apply(L, xx, y, i, [&](int fld, int64_t j) { return xi[fld * n + j]; }, a0, a1, a2);
+    for (int c = threadIdx.x; c < GT_Y * GT_X; c += NT) {
+        const int ly = c / GT_X, lx = c - ly * GT_X, gy = y0 + ly, gx = x0 + lx;
+        if (gx >= w || gy >= h) continue;
+        const int64_t i = (int64_t)gy * w + gx;
+        double a0, a1, a2, v0, v1, v2, z0, z1, z2;
+        mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0, a1, a2,
+                   v0, v1, v2);
         const double f0 = f[i], f1 = f[n + i], f2v = f[2 * n + i];
         mg_dinv(L, i, f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
-        const double o0 = xi[i] + MG_OMEGA * z0, o1 = xi[n + i] + MG_OMEGA * z1, o2 = xi[2 * n + i] + MG_OMEGA * z2;
-        xo[i] = o0;
-        xo[n + i] = o1;
-        xo[2 * n + i] = o2;
-        rz = f0 * o0 + f1 * o1 + f2v * o2;
+        const double o0 = v0 + MG_OMEGA * z0, o1 = v1 + MG_OMEGA * z1, o2 = v2 + MG_OMEGA * z2;
+        out[i] = o0;
+        out[n + i] = o1;
+        out[2 * n + i] = o2;
+        rz += f0 * o0 + f1 * o1 + f2v * o2;
     }
-    if constexpr (RZ) {
-        double v[1] = {rz}, tot[1];
-        if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rz[1] = tot[0];
-    }
+    if constexpr (RZ) mg_block_partial(rz, rz_part);
 }
 
 // coarsest level: MG_CSWEEPS damped block-Jacobi sweeps from zero in one block (x in LDS, each
 // thread's cell coefficients in registers: a sweep touches no global memory);
-// RZ (single-level hierarchy): also f . x -> gath_rz[1]
+// RZ (single-level hierarchy): also the partial f . x -> rz_part[0]
 template <bool RZ>
 __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, const double* __restrict__ f,
-                                                     double* __restrict__ xout, double* gath_rz) {
+                                                     double* __restrict__ xout, double* rz_part) {
     if (S->done) return;
     __shared__ double xs[2][3 * MG_COARSE];
     __shared__ double red[16];
@@ -643,143 +837,83 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, co
         if (threadIdx.x == 0) {
             double s = 0.0;
             for (int w = 0; w < 16; ++w) s += red[w];
-            gath_rz[1] = s;
+            rz_part[0] = s;
         }
     }
 }
 
-// PCG pieces without the block-Jacobi preconditioner (the V-cycle supplies z):
-// init: r = b, r.r -> gath_rz[0]; upd: x += alpha p, r -= alpha A p, r.r -> gath_rz[0]
-__global__ __launch_bounds__(NT) void k_gn_mg_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
-                                                   RedBuf rb, double* gath_rz) {
-    double rr = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < 3 * n; i += (int64_t)gridDim.x * NT) {
-        const double v = b[i];
-        r[i] = v;
-        rr += v * v;
-    }
-    double v[1] = {rr}, tot[1];
-    if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rz[0] = tot[0];
-}
+}  // namespace foto
 
-__global__ __launch_bounds__(NT) void k_gn_mg_upd(int w, int h, const double* __restrict__ fx,
-                                                  const double* __restrict__ fy, const double* __restrict__ f2,
-                                                  double a, double l, const double* __restrict__ p,
-                                                  double* __restrict__ x, double* __restrict__ r, CGScal* S,
-                                                  RedBuf rb, const double* __restrict__ gath_pq,
-                                                  double* __restrict__ gath_rz) {
-    if (S->done) return;
-    const int k = S->pad[0];
-    const double alpha = S->rho / gath_pq[0];
-    const int64_t n = (int64_t)w * h;
-    double rr = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-        const GNPix P = gn_pix(w, h, i);
-        double qu, qv, qm;
-        gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, [&](int f, int64_t j) { return p[f * n + j]; }, qu, qv, qm);
-        const double q3[3] = {qu, qv, qm};
-#pragma unroll
-        for (int f = 0; f < 3; ++f) {
-            const int64_t o = f * n + i;
-            const double ap = alpha * p[o];
-            x[o] = (k == 0) ? 0.0 + ap : x[o] + ap;
-            const double rn = r[o] - alpha * q3[f];
-            r[o] = rn;
-            rr += rn * rn;
-        }
-    }
-    double v[1] = {rr}, tot[1];
-    if (gn_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) {
-        gath_rz[0] = tot[0];
-        S->pad[0] = k + 1;   // iteration index kept on the device (graph replays carry none)
-    }
-}
+// ============================================================================ GN plan (host)
 
-// ---------------------------------------------------------------------------- host side
+using namespace foto;
 
-int GnMG::setup(int w, int h, const double* fx, const double* fy, const double* f2, double alpha, double lam,
-                hipStream_t s) {
-    free_all();
-    int lw = w, lh = h;
-    double sc = 1.0;
-    size_t total = 0;
-    for (;;) {   // level geometry first, then one allocation for the whole hierarchy
-        Lev L;
-        L.w = lw;
-        L.h = lh;
-        L.s[0] = alpha * sc; L.s[1] = alpha * sc; L.s[2] = lam * sc;
-        total += 24 * (size_t)lw * lh;
-        lev.push_back(L);
-        if ((int64_t)lw * lh <= MG_COARSE) break;
-        lw = (lw + 1) / 2;
-        lh = (lh + 1) / 2;
-        sc *= 0.25;
-    }
+struct foto_gn_plan {
+    int w = 0, h = 0, maxiter = 0;
+    double alpha = 0, lam = 0, rtol = 0;
+    hipStream_t s = nullptr;
     double* base = nullptr;
-    FOTO_TRY(alloc(total, &base));
-    for (Lev& L : lev) {
-        const size_t n = (size_t)L.w * L.h;
-        L.B = base; base += 6 * n;
-        L.Dinv = base; base += 6 * n;
-        L.f = base; base += 3 * n;
-        L.x = base; base += 3 * n;
-        L.y = base; base += 3 * n;
-        L.r = base; base += 3 * n;
-    }
-    const int64_t n0 = (int64_t)w * h;
-    k_mg_b0<<<flat_blocks(n0), NT, 0, s>>>(n0, fx, fy, f2, lev[0].B);
-    FOTO_HIP_CHECK(hipGetLastError());
-    for (size_t l = 1; l < lev.size(); ++l) {
-        const int64_t nc = (int64_t)lev[l].w * lev[l].h;
-        k_mg_coarsen<<<flat_blocks(nc), NT, 0, s>>>(lev[l - 1].w, lev[l - 1].h, lev[l - 1].B, lev[l].w, lev[l].h,
-                                                   lev[l].B);
-        FOTO_HIP_CHECK(hipGetLastError());
-    }
-    for (size_t l = 0; l < lev.size(); ++l) {
-        const int64_t n = (int64_t)lev[l].w * lev[l].h;
-        k_mg_dinv<<<flat_blocks(n), NT, 0, s>>>(desc(l), lev[l].Dinv);
-        FOTO_HIP_CHECK(hipGetLastError());
-    }
-    return 0;
-}
+    double *d1 = nullptr, *d2 = nullptr, *fx = nullptr, *fy = nullptr, *ft = nullptr, *b = nullptr, *x = nullptr,
+           *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr;
+    double *rr_part = nullptr, *pq_part = nullptr, *rz_part[2] = {nullptr, nullptr};
+    int nb_pix = 0, nb_rz = 0;
+    CGScal* dS = nullptr;
+    CGScal* hS = nullptr;
+    struct Lev {
+        int w = 0, h = 0;
+        double s[3] = {0, 0, 0};
+        double *B = nullptr, *Dinv = nullptr, *f = nullptr, *x = nullptr, *y = nullptr;
+    };
+    std::vector<Lev> lev;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    int last_its = 0;
+    double last[4] = {0, 0, 0, 0};   // ms setup+upload, ms PCG, iterations, iterations launched
 
-MGLev GnMG::desc(size_t l) const {
-    const Lev& L = lev[l];
-    return MGLev{L.w, L.h, L.s[0], L.s[1], L.s[2], L.B, L.Dinv};
-}
+    MGLev desc(size_t l) const {
+        const Lev& L = lev[l];
+        return MGLev{L.w, L.h, L.s[0], L.s[1], L.s[2], L.B, L.Dinv};
+    }
+    ~foto_gn_plan() {
+        if (s) (void)hipStreamSynchronize(s);
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        if (graph) (void)hipGraphDestroy(graph);
+        for (auto e : ev) if (e) (void)hipEventDestroy(e);
+        if (base) (void)hipFree(base);
+        if (hS) (void)hipHostFree(hS);
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
 
-// z = V(r); r.z -> gath_rz[1]
-int GnMG::vcycle(const double* r, double* z, const CGScal* S, RedBuf rb, double* gath_rz, hipStream_t s) {
-    const size_t nl = lev.size();
+namespace foto {
+
+// z = V(r) and the partials of r.z -> rz_out
+static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out) {
+    hipStream_t s = P->s;
+    const size_t nl = P->lev.size();
     if (nl == 1) {
-        k_mg_coarse<true><<<1, 1024, 0, s>>>(desc(0), S, r, z, gath_rz);
+        k_mg_coarse<true><<<1, 1024, 0, s>>>(P->desc(0), P->dS, r, z, rz_out);
         FOTO_HIP_CHECK(hipGetLastError());
         return 0;
     }
-    // down
     for (size_t l = 0; l + 1 < nl; ++l) {
-        const Lev& L = lev[l];
-        const int64_t n = (int64_t)L.w * L.h, nc = (int64_t)lev[l + 1].w * lev[l + 1].h;
-        const double* f = (l == 0) ? r : L.f;
-        k_mg_down<<<flat_blocks(n), NT, 0, s>>>(desc(l), S, f, L.x, L.r);
-        FOTO_HIP_CHECK(hipGetLastError());
-        k_mg_restrict<<<flat_blocks(nc), NT, 0, s>>>(L.w, L.h, S, L.r, lev[l + 1].w, lev[l + 1].h, lev[l + 1].f);
+        const auto& L = P->lev[l];
+        const auto& C = P->lev[l + 1];
+        k_mg_down2<<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x, C.f);
         FOTO_HIP_CHECK(hipGetLastError());
     }
     const size_t c = nl - 1;
-    k_mg_coarse<false><<<1, 1024, 0, s>>>(desc(c), S, lev[c].f, lev[c].x, nullptr);
+    k_mg_coarse<false><<<1, 1024, 0, s>>>(P->desc(c), P->dS, P->lev[c].f, P->lev[c].x, nullptr);
     FOTO_HIP_CHECK(hipGetLastError());
-    // up: the coarser level's correction sits in its x (coarsest) or y (post-smoothed)
-    const double* e = lev[c].x;
+    const double* e = P->lev[c].x;
     for (size_t l = nl - 1; l-- > 0;) {
-        const Lev& L = lev[l];
-        const int64_t n = (int64_t)L.w * L.h;
-        k_mg_prolong<<<flat_blocks(n), NT, 0, s>>>(L.w, L.h, S, e, lev[l + 1].w, lev[l + 1].h, L.x);
-        FOTO_HIP_CHECK(hipGetLastError());
+        const auto& L = P->lev[l];
+        const auto& C = P->lev[l + 1];
         if (l == 0) {
-            k_mg_smooth<true><<<flat_blocks(n), NT, 0, s>>>(desc(0), S, r, L.x, z, rb, gath_rz);
+            k_mg_up2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(0), C.w, C.h, P->dS, e, r, L.x, z, rz_out);
         } else {
-            k_mg_smooth<false><<<flat_blocks(n), NT, 0, s>>>(desc(l), S, L.f, L.x, L.y, rb, nullptr);
+            k_mg_up2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, e, L.f, L.x, L.y, nullptr);
             e = L.y;
         }
         FOTO_HIP_CHECK(hipGetLastError());
@@ -787,30 +921,165 @@ int GnMG::vcycle(const double* r, double* z, const CGScal* S, RedBuf rb, double*
     return 0;
 }
 
-int GnMG::alloc(size_t n_doubles, double** p) {
-    FOTO_HIP_CHECK(hipMalloc((void**)p, std::max<size_t>(n_doubles, 1) * sizeof(double)));
-    bufs.push_back(*p);
+// PCG iteration of parity `par` (k even: p0 -> p1, z_k's r.z in rz_part[0])
+static int gn_iteration(foto_gn_plan* P, int par) {
+    const int w = P->w, h = P->h;
+    double* po = par ? P->p1 : P->p0;
+    double* pn = par ? P->p0 : P->p1;
+    const double* rzc = P->rz_part[par];
+    const double* rzp = P->rz_part[par ^ 1];
+    k_gnp_dir<<<P->nb_pix, NT, 0, P->s>>>(w, h, P->fx, P->fy, P->d2, P->alpha, P->lam, P->z, po, pn, P->dS,
+                                           P->rr_part, P->nb_pix, rzc, rzp, P->nb_rz, P->pq_part, P->rtol);
+    FOTO_HIP_CHECK(hipGetLastError());
+    k_gnp_upd<<<P->nb_pix, NT, 0, P->s>>>(w, h, P->fx, P->fy, P->d2, P->alpha, P->lam, pn, P->x, P->r, P->dS, rzc,
+                                           P->nb_rz, P->pq_part, P->nb_pix, P->rr_part);
+    FOTO_HIP_CHECK(hipGetLastError());
+    return gn_vcycle(P, P->r, P->z, P->rz_part[par ^ 1]);
+}
+
+static int gn_plan_init(foto_gn_plan* P) {
+    const int w = P->w, h = P->h;
+    const size_t n = (size_t)w * h;
+    FOTO_HIP_CHECK(hipStreamCreateWithFlags(&P->s, hipStreamNonBlocking));
+    for (auto& e : P->ev) FOTO_HIP_CHECK(hipEventCreate(&e));
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
+    P->nb_pix = flat_blocks((int64_t)n);
+    // level geometry
+    int lw = w, lh = h;
+    double sc = 1.0;
+    size_t lev_total = 0;
+    for (;;) {
+        foto_gn_plan::Lev L;
+        L.w = lw; L.h = lh;
+        L.s[0] = P->alpha * sc; L.s[1] = P->alpha * sc; L.s[2] = P->lam * sc;
+        lev_total += 21 * (size_t)lw * lh;
+        P->lev.push_back(L);
+        if ((int64_t)lw * lh <= MG_COARSE) break;
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+        sc *= 0.25;
+    }
+    P->nb_rz = P->lev.size() == 1 ? 1 : mg_tiles(w, h);
+    const size_t nscal = sizeof(CGScal) / sizeof(double) + 1;
+    const size_t total = 23 * n + lev_total + 2 * (size_t)P->nb_pix + 2 * (size_t)P->nb_rz + nscal + 64;
+    FOTO_HIP_CHECK(hipMalloc((void**)&P->base, total * sizeof(double)));
+    double* q = P->base;
+    P->d1 = q; q += n; P->d2 = q; q += n; P->fx = q; q += n; P->fy = q; q += n; P->ft = q; q += n;
+    P->b = q; q += 3 * n; P->x = q; q += 3 * n; P->r = q; q += 3 * n; P->z = q; q += 3 * n;
+    P->p0 = q; q += 3 * n; P->p1 = q; q += 3 * n;
+    for (auto& L : P->lev) {
+        const size_t m = (size_t)L.w * L.h;
+        L.B = q; q += 6 * m; L.Dinv = q; q += 6 * m; L.f = q; q += 3 * m; L.x = q; q += 3 * m; L.y = q; q += 3 * m;
+    }
+    P->rr_part = q; q += P->nb_pix;
+    P->pq_part = q; q += P->nb_pix;
+    P->rz_part[0] = q; q += P->nb_rz;
+    P->rz_part[1] = q; q += P->nb_rz;
+    P->dS = (CGScal*)q;
+    // two iterations (p0 -> p1 -> p0) captured once; the kernels read the iteration index from
+    // the device, so the graph is replayed unchanged
+    FOTO_HIP_CHECK(hipStreamBeginCapture(P->s, hipStreamCaptureModeThreadLocal));
+    const int c1 = gn_iteration(P, 0), c2 = c1 < 0 ? c1 : gn_iteration(P, 1);
+    const hipError_t ec = hipStreamEndCapture(P->s, &P->graph);
+    FOTO_TRY(c2);
+    FOTO_HIP_CHECK(ec);
+    FOTO_HIP_CHECK(hipGraphInstantiate(&P->gexec, P->graph, nullptr, nullptr, 0));
     return 0;
 }
 
-void GnMG::free_all() {
-    for (void* p : bufs) (void)hipFree(p);
-    bufs.clear();
-    lev.clear();
-}
-
-hipError_t launch_gn_mg_init(int64_t n, const double* b, double* r, RedBuf rb, double* gath_rz, hipStream_t s) {
-    // grid sized by n (not 3 n): the reduction scratch holds 2 partials per block of n
-    k_gn_mg_init<<<gn_grid(n), NT, 0, s>>>(n, b, r, rb, gath_rz);
-    return hipGetLastError();
-}
-
-hipError_t launch_gn_mg_upd(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
-                            double lam, const double* p, double* x, double* r, CGScal* S, RedBuf rb,
-                            const double* gath_pq, double* gath_rz, hipStream_t s) {
-    k_gn_mg_upd<<<gn_grid((int64_t)w * h), NT, 0, s>>>(w, h, fx, fy, f2, alpha, lam, p, x, r, S, rb, gath_pq,
-                                                         gath_rz);
-    return hipGetLastError();
+static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, double* u, double* v, double* m,
+                         int* iterations) {
+    const int w = P->w, h = P->h;
+    const int64_t n = (int64_t)w * h;
+    hipStream_t s = P->s;
+    FOTO_HIP_CHECK(hipEventRecord(P->ev[0], s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, f1, n * sizeof(double), hipMemcpyHostToDevice, s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, f2, n * sizeof(double), hipMemcpyHostToDevice, s));
+    FOTO_HIP_CHECK(hipMemsetAsync(P->dS, 0, sizeof(CGScal), s));
+    FOTO_HIP_CHECK(hipMemsetAsync(P->x, 0, 3 * n * sizeof(double), s));
+    FOTO_HIP_CHECK(launch_gn_coeffs(w, h, P->d1, P->d2, P->fx, P->fy, P->ft, s));
+    FOTO_HIP_CHECK(launch_gn_rhs(w, h, P->fx, P->fy, P->d2, P->ft, P->b, s));
+    // image-dependent multigrid coefficients
+    k_mg_b0<<<flat_blocks(n), NT, 0, s>>>(n, P->fx, P->fy, P->d2, P->lev[0].B);
+    FOTO_HIP_CHECK(hipGetLastError());
+    for (size_t l = 1; l < P->lev.size(); ++l) {
+        const auto& L = P->lev[l - 1];
+        const auto& C = P->lev[l];
+        k_mg_coarsen<<<flat_blocks((int64_t)C.w * C.h), NT, 0, s>>>(L.w, L.h, L.B, C.w, C.h, C.B);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    for (size_t l = 0; l < P->lev.size(); ++l) {
+        k_mg_dinv<<<flat_blocks((int64_t)P->lev[l].w * P->lev[l].h), NT, 0, s>>>(P->desc(l), P->lev[l].Dinv);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
+    // r = b, r.r; z_0 = V(r), r.z -> rz_part[0]
+    k_gnp_init<<<P->nb_pix, NT, 0, s>>>(n, P->b, P->r, P->rr_part);
+    FOTO_HIP_CHECK(hipGetLastError());
+    FOTO_TRY(gn_vcycle(P, P->r, P->z, P->rz_part[0]));
+    FOTO_HIP_CHECK(hipEventRecord(P->ev[1], s));
+    // replay pairs of iterations; the first wait comes after the previous solve's count
+    int k = 0;
+    bool done = false;
+    const int maxiter = P->maxiter;
+    const int first = P->last_its > 0 ? P->last_its + (P->last_its & 1) : 16;
+    while (k < maxiter) {
+        const int chunk = std::min(k == 0 ? first : 2, maxiter - k);
+        int j = 0;
+        for (; j + 2 <= chunk; j += 2, k += 2) FOTO_HIP_CHECK(hipGraphLaunch(P->gexec, s));
+        if (j < chunk) {   // odd maxiter: one last iteration outside the graph (k even: p0 -> p1)
+            FOTO_TRY(gn_iteration(P, 0));
+            ++k;
+        }
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->hS, P->dS, sizeof(CGScal), hipMemcpyDeviceToHost, s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        if (P->hS->done) { done = true; break; }
+    }
+    FOTO_HIP_CHECK(hipEventRecord(P->ev[2], s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(u, P->x, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(v, P->x + n, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(m, P->x + 2 * n, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    const int its = done ? P->hS->iters : maxiter;
+    float t0 = 0.f, t1 = 0.f;
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t0, P->ev[0], P->ev[1]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t1, P->ev[1], P->ev[2]));
+    P->last[0] = t0; P->last[1] = t1; P->last[2] = its; P->last[3] = k;
+    P->last_its = done ? its : 0;
+    if (iterations) *iterations = its;
+    return done ? 0 : maxiter;
 }
 
 }  // namespace foto
+
+extern "C" {
+
+int foto_gn_plan_create(int w, int h, double alpha, double lambda_, double rtol, int maxiter, foto_gn_plan** out) {
+    if (!out) { set_error("null argument"); return FOTO_ERR_ARG; }
+    if (w < 2 || h < 2) { set_error("w = %d, h = %d: GN needs >= 2 pixels per axis", w, h); return FOTO_ERR_ARG; }
+    if (!(alpha > 0) || !(lambda_ > 0)) {
+        set_error("GN needs alpha > 0 and lambda > 0 (the block-Jacobi smoother divides by them)");
+        return FOTO_ERR_ARG;
+    }
+    if (maxiter < 0) { set_error("maxiter < 0"); return FOTO_ERR_ARG; }
+    auto P = std::make_unique<foto_gn_plan>();
+    P->w = w; P->h = h; P->alpha = alpha; P->lam = lambda_; P->rtol = rtol; P->maxiter = maxiter;
+    FOTO_TRY(gn_plan_init(P.get()));
+    *out = P.release();
+    return 0;
+}
+
+int foto_gn_plan_solve(foto_gn_plan* p, const double* f1, const double* f2, double* u, double* v, double* m,
+                       int* iterations) {
+    if (!p || !f1 || !f2 || !u || !v || !m) { set_error("null argument"); return FOTO_ERR_ARG; }
+    return gn_plan_solve(p, f1, f2, u, v, m, iterations);
+}
+
+int foto_gn_plan_timing(const foto_gn_plan* p, double* out4) {
+    if (!p || !out4) { set_error("null argument"); return FOTO_ERR_ARG; }
+    for (int k = 0; k < 4; ++k) out4[k] = p->last[k];
+    return 0;
+}
+
+void foto_gn_plan_destroy(foto_gn_plan* p) { delete p; }
+
+}  // extern "C"

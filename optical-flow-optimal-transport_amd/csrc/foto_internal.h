@@ -224,27 +224,4 @@ hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double
                              double alpha, double lam, const double* p, double* x, double* r, double* z,
                              CGScal* S, RedBuf rb, const double* gath_pq, double* gath_rz, hipStream_t s);
 
-// GN multigrid preconditioner (foto_gn.hip): one symmetric V-cycle z = V(r), r.z -> gath_rz[1]
-struct MGLev;
-struct GnMG {
-    struct Lev {
-        int w = 0, h = 0;
-        double s[3] = {0, 0, 0};
-        double *B = nullptr, *Dinv = nullptr, *f = nullptr, *x = nullptr, *y = nullptr, *r = nullptr;
-    };
-    std::vector<Lev> lev;
-    std::vector<void*> bufs;
-    int setup(int w, int h, const double* fx, const double* fy, const double* f2, double alpha, double lam,
-              hipStream_t s);
-    int vcycle(const double* r, double* z, const CGScal* S, RedBuf rb, double* gath_rz, hipStream_t s);
-    MGLev desc(size_t l) const;
-    int alloc(size_t n_doubles, double** p);
-    void free_all();
-    ~GnMG() { free_all(); }
-};
-hipError_t launch_gn_mg_init(int64_t n, const double* b, double* r, RedBuf rb, double* gath_rz, hipStream_t s);
-hipError_t launch_gn_mg_upd(int w, int h, const double* fx, const double* fy, const double* f2, double alpha,
-                            double lam, const double* p, double* x, double* r, CGScal* S, RedBuf rb,
-                            const double* gath_pq, double* gath_rz, hipStream_t s);
-
 }  // namespace foto

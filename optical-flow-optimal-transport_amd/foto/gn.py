@@ -34,3 +34,49 @@ def solve(f1, f2, w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
     info = check(lib().foto_gn_solve(dptr(a), dptr(b), w, h, float(alpha), float(lam), float(rtol), int(maxiter),
                                      dptr(u), dptr(v), dptr(m), ctypes.byref(its)))
     return u, v, m, info, its.value
+
+
+class Plan:
+    """A reusable GN solver for one (w, h, alpha, lambda): classical.GLLOpticalFlow after
+    setAlpha/setLambda (classical.py:25-66).  Buffers, the multigrid hierarchy and the replayed
+    PCG graph are made once; solve(f1, f2) is one process() (classical.py:68-130)."""
+
+    def __init__(self, w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
+        self.w, self.h, self.alpha, self.lam = int(w), int(h), float(alpha), float(lam)
+        self._p = ctypes.c_void_p()
+        check(lib().foto_gn_plan_create(self.w, self.h, self.alpha, self.lam, float(rtol), int(maxiter),
+                                        ctypes.byref(self._p)))
+
+    def solve(self, f1, f2):
+        """Returns (u, v, m, info, iterations), like solve()."""
+        n = self.w * self.h
+        a, b = f64(f1, n, "f1"), f64(f2, n, "f2")
+        u, v, m = np.empty(n), np.empty(n), np.empty(n)
+        its = ctypes.c_int(0)
+        info = check(lib().foto_gn_plan_solve(self._p, dptr(a), dptr(b), dptr(u), dptr(v), dptr(m),
+                                              ctypes.byref(its)))
+        return u, v, m, info, its.value
+
+    def timing(self):
+        """{ms_setup, ms_pcg, iterations, launched} of the last solve (device events)."""
+        out = np.zeros(4)
+        check(lib().foto_gn_plan_timing(self._p, dptr(out)))
+        return {"ms_setup": float(out[0]), "ms_pcg": float(out[1]), "iterations": int(out[2]),
+                "launched": int(out[3])}
+
+    def close(self):
+        if self._p:
+            lib().foto_gn_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

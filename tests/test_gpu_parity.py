@@ -453,14 +453,37 @@ def test_gn_solve(gold):
 def test_gn_solve_multilevel(pair, monkeypatch):
     """GN at 160x120 -- a four-level V-cycle (160x120 .. 20x15), which the goldens (40x30,
     17x13: two levels / coarse solve only) do not reach -- against the oracle's spsolve
-    (SuperLU, classical.py:126), with the graph-replayed and the directly launched iteration."""
+    (SuperLU, classical.py:126), with the multigrid PCG (default) and the block-Jacobi PCG."""
     from foto.synthetic import sinusoid_pair, textured_pair
     w, h, alpha, lam = 160, 120, 0.1, 0.2
     f1, f2 = (sinusoid_pair if pair == "sinusoid" else textured_pair)(w, h)
     ref = O.gn_solve(f1, f2, w, h, alpha, lam)
-    for graph in ("1", "0"):
-        monkeypatch.setenv("FOTO_GN_GRAPH", graph)
+    for mg, cap in (("1", 100), ("0", 5000)):
+        monkeypatch.setenv("FOTO_GN_MG", mg)
         u, v, m, info, its = gn.solve(f1, f2, w, h, alpha, lam)
-        assert info == 0 and 0 < its < 100
+        print(f"{pair} FOTO_GN_MG={mg}: {its} PCG its")
+        assert info == 0 and 0 < its < cap
         for a, b in zip((u, v, m), ref):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * max(1.0, np.abs(b).max()))
+
+
+def test_gn_plan_reuse():
+    """One gn.Plan (classical.GLLOpticalFlow after setAlpha/setLambda) solving pairs in turn:
+    every solve equals the one-shot foto_gn_solve bit for bit (same kernels, same graph), the
+    first wait of a reused plan comes after the previous solve's count (over- and
+    under-predicted here: the two pairs need different counts), and a truncated solve
+    (odd maxiter: the last iteration outside the graph) returns info = maxiter."""
+    from foto.synthetic import sinusoid_pair, textured_pair
+    w, h, alpha, lam = 96, 72, 0.1, 0.2
+    pairs = [sinusoid_pair(w, h), textured_pair(w, h)]
+    one = [gn.solve(f1, f2, w, h, alpha, lam) for f1, f2 in pairs]
+    with gn.Plan(w, h, alpha, lam) as P:
+        for j in (0, 1, 0, 1):
+            u, v, m, info, its = P.solve(*pairs[j])
+            t = P.timing()
+            assert info == 0 and its == one[j][4] and t["iterations"] == its and t["launched"] >= its
+            for a, b in zip((u, v, m), one[j][:3]):
+                np.testing.assert_array_equal(a, b)
+    with gn.Plan(w, h, alpha, lam, maxiter=5) as P:
+        u, v, m, info, its = P.solve(*pairs[0])
+        assert info == 5 and its == 5

@@ -5,7 +5,7 @@
 # usage: tools/profile_round.sh TAG [bench args...]      (run from the repo root on the GPU box)
 set -o pipefail
 tag="$1"; shift
-args="${*:---steps 10 --warmup 2 --no-cpu-baseline}"
+args="${*:---steps 10 --warmup 2 --no-cpu-baseline --no-stencil}"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out
 rm -rf $O/prof_kt $O/prof_fetch $O/prof_write $O/cal_fetch $O/cal_write
