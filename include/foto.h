@@ -154,8 +154,9 @@ int foto_gn_apply(const double* f1, const double* f2, int w, int h, double alpha
 int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
 /* process(): spsolve replaced by CG preconditioned by a multigrid V-cycle (block-Jacobi
  * smoothing, FOTO_GN_MG=0: plain block-Jacobi PCG) to rtol (default 1e-10).
- * Returns 0 (converged) or maxiter (not converged), < 0 on error.  One-shot: a plan is made,
- * used once and destroyed.                                                        */
+ * Returns 0 (converged) or maxiter (not converged), < 0 on error.  Runs on a plan (below)
+ * cached per process for the last (w, h, alpha, lambda, rtol, maxiter, device), as FFT
+ * libraries cache plans; FOTO_GN_PLAN_CACHE=0 makes and destroys one per call.       */
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   double rtol, int maxiter, double* u, double* v, double* m, int* iterations);
 
@@ -171,6 +172,8 @@ int foto_gn_plan_solve(foto_gn_plan* p, const double* f1, const double* f2, doub
 /* the last solve: {ms upload + setup + V-cycle of r0, ms PCG iterations (device events),
  * iterations, iterations launched}                                                */
 int foto_gn_plan_timing(const foto_gn_plan* p, double* out4);
+/* the device the plan was made on (-1 for NULL)                                    */
+int foto_gn_plan_device(const foto_gn_plan* p);
 void foto_gn_plan_destroy(foto_gn_plan* p);
 
 /* ------------------------------------------------------------------ evaluation

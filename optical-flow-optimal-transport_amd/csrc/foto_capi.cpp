@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <mutex>
 
 #include "foto_internal.h"
 
@@ -286,11 +287,31 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
     if (maxiter < 0) { set_error("maxiter < 0"); return FOTO_ERR_ARG; }
     const char* emg = getenv("FOTO_GN_MG");   // 0: 3x3 block-Jacobi preconditioner (A/B runs)
     if (!(emg && atoi(emg) == 0)) {
-        // multigrid-preconditioned CG through a one-shot plan (foto_gn.hip)
-        foto_gn_plan* P = nullptr;
-        FOTO_TRY(foto_gn_plan_create(w, h, alpha, lam, rtol, maxiter, &P));
-        std::unique_ptr<foto_gn_plan, void (*)(foto_gn_plan*)> pg(P, foto_gn_plan_destroy);
-        return foto_gn_plan_solve(P, f1, f2, u, v, m, iterations);
+        // multigrid-preconditioned CG through a plan (foto_gn.hip), cached per process like an
+        // FFT plan: a call with the same (w, h, alpha, lambda, rtol, maxiter) as the previous
+        // one reuses its buffers and graph (FOTO_GN_PLAN_CACHE=0: make and destroy a plan per call)
+        const char* ec = getenv("FOTO_GN_PLAN_CACHE");
+        const bool cache = !(ec && atoi(ec) == 0);
+        // (the cached plan is never destroyed at process exit: the HIP runtime may be gone by then)
+        static std::mutex mu;
+        static foto_gn_plan* cached = nullptr;
+        static double key[6] = {0, 0, 0, 0, 0, 0};
+        const double k6[6] = {(double)w, (double)h, alpha, lam, rtol, (double)maxiter};
+        std::lock_guard<std::mutex> lk(mu);
+        int dev = 0;
+        FOTO_HIP_CHECK(hipGetDevice(&dev));
+        if (!cache || !cached || memcmp(key, k6, sizeof(k6)) != 0 || foto_gn_plan_device(cached) != dev) {
+            foto_gn_plan_destroy(cached);
+            cached = nullptr;
+            FOTO_TRY(foto_gn_plan_create(w, h, alpha, lam, rtol, maxiter, &cached));
+            memcpy(key, k6, sizeof(k6));
+        }
+        const int rc = foto_gn_plan_solve(cached, f1, f2, u, v, m, iterations);
+        if (!cache || rc < 0) {
+            foto_gn_plan_destroy(cached);
+            cached = nullptr;
+        }
+        return rc;
     }
     // 3x3 block-Jacobi PCG (the first GPU version; kept for A/B runs)
     Scope S;

@@ -12,6 +12,7 @@
 #include "foto_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -836,7 +837,7 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, co
         __syncthreads();
         if (threadIdx.x == 0) {
             double s = 0.0;
-            for (int w = 0; w < 16; ++w) s += red[w];
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
             rz_part[0] = s;
         }
     }
@@ -849,7 +850,7 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, co
 using namespace foto;
 
 struct foto_gn_plan {
-    int w = 0, h = 0, maxiter = 0;
+    int w = 0, h = 0, maxiter = 0, device = 0;
     double alpha = 0, lam = 0, rtol = 0;
     hipStream_t s = nullptr;
     double* base = nullptr;
@@ -859,6 +860,8 @@ struct foto_gn_plan {
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
     CGScal* hS = nullptr;
+    double* hbuf = nullptr;   // pinned staging: f1, f2, u, v, m (pageable copies of ~2.5 MB were
+                              // pinned on the fly by the runtime: 15-25 ms per solve at 640x480)
     struct Lev {
         int w = 0, h = 0;
         double s[3] = {0, 0, 0};
@@ -882,18 +885,26 @@ struct foto_gn_plan {
         for (auto e : ev) if (e) (void)hipEventDestroy(e);
         if (base) (void)hipFree(base);
         if (hS) (void)hipHostFree(hS);
+        if (hbuf) (void)hipHostFree(hbuf);
         if (s) (void)hipStreamDestroy(s);
     }
 };
 
 namespace foto {
 
+// one thread per cell of the coarsest level, whole waves (fewer waves: cheaper barriers
+// between the sweeps)
+static int mg_coarse_threads(const foto_gn_plan::Lev& L) {
+    const int n = L.w * L.h;
+    return std::min(1024, ((n + 63) / 64) * 64);
+}
+
 // z = V(r) and the partials of r.z -> rz_out
 static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out) {
     hipStream_t s = P->s;
     const size_t nl = P->lev.size();
     if (nl == 1) {
-        k_mg_coarse<true><<<1, 1024, 0, s>>>(P->desc(0), P->dS, r, z, rz_out);
+        k_mg_coarse<true><<<1, mg_coarse_threads(P->lev[0]), 0, s>>>(P->desc(0), P->dS, r, z, rz_out);
         FOTO_HIP_CHECK(hipGetLastError());
         return 0;
     }
@@ -904,7 +915,8 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
         FOTO_HIP_CHECK(hipGetLastError());
     }
     const size_t c = nl - 1;
-    k_mg_coarse<false><<<1, 1024, 0, s>>>(P->desc(c), P->dS, P->lev[c].f, P->lev[c].x, nullptr);
+    k_mg_coarse<false><<<1, mg_coarse_threads(P->lev[c]), 0, s>>>(P->desc(c), P->dS, P->lev[c].f, P->lev[c].x,
+                                                                  nullptr);
     FOTO_HIP_CHECK(hipGetLastError());
     const double* e = P->lev[c].x;
     for (size_t l = nl - 1; l-- > 0;) {
@@ -940,9 +952,11 @@ static int gn_iteration(foto_gn_plan* P, int par) {
 static int gn_plan_init(foto_gn_plan* P) {
     const int w = P->w, h = P->h;
     const size_t n = (size_t)w * h;
+    FOTO_HIP_CHECK(hipGetDevice(&P->device));
     FOTO_HIP_CHECK(hipStreamCreateWithFlags(&P->s, hipStreamNonBlocking));
     for (auto& e : P->ev) FOTO_HIP_CHECK(hipEventCreate(&e));
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hbuf, 5 * n * sizeof(double)));
     P->nb_pix = flat_blocks((int64_t)n);
     // level geometry
     int lw = w, lh = h;
@@ -993,8 +1007,11 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     const int64_t n = (int64_t)w * h;
     hipStream_t s = P->s;
     FOTO_HIP_CHECK(hipEventRecord(P->ev[0], s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, f1, n * sizeof(double), hipMemcpyHostToDevice, s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, f2, n * sizeof(double), hipMemcpyHostToDevice, s));
+    double* hb = P->hbuf;
+    memcpy(hb, f1, n * sizeof(double));
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, hb, n * sizeof(double), hipMemcpyHostToDevice, s));
+    memcpy(hb + n, f2, n * sizeof(double));
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, hb + n, n * sizeof(double), hipMemcpyHostToDevice, s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->dS, 0, sizeof(CGScal), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->x, 0, 3 * n * sizeof(double), s));
     FOTO_HIP_CHECK(launch_gn_coeffs(w, h, P->d1, P->d2, P->fx, P->fy, P->ft, s));
@@ -1035,10 +1052,11 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
         if (P->hS->done) { done = true; break; }
     }
     FOTO_HIP_CHECK(hipEventRecord(P->ev[2], s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(u, P->x, n * sizeof(double), hipMemcpyDeviceToHost, s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(v, P->x + n, n * sizeof(double), hipMemcpyDeviceToHost, s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(m, P->x + 2 * n, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(hb + 2 * n, P->x, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s));
     FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    memcpy(u, hb + 2 * n, n * sizeof(double));
+    memcpy(v, hb + 3 * n, n * sizeof(double));
+    memcpy(m, hb + 4 * n, n * sizeof(double));
     const int its = done ? P->hS->iters : maxiter;
     float t0 = 0.f, t1 = 0.f;
     FOTO_HIP_CHECK(hipEventElapsedTime(&t0, P->ev[0], P->ev[1]));
@@ -1079,6 +1097,8 @@ int foto_gn_plan_timing(const foto_gn_plan* p, double* out4) {
     for (int k = 0; k < 4; ++k) out4[k] = p->last[k];
     return 0;
 }
+
+int foto_gn_plan_device(const foto_gn_plan* p) { return p ? p->device : -1; }
 
 void foto_gn_plan_destroy(foto_gn_plan* p) { delete p; }
 

@@ -99,6 +99,7 @@ SIGNATURES = {
     "foto_gn_plan_create": (_I, [_I, _I, _Dbl, _Dbl, _Dbl, _I, ctypes.POINTER(_P)]),
     "foto_gn_plan_solve": (_I, [_P, _D, _D, _D, _D, _D, ctypes.POINTER(_I)]),
     "foto_gn_plan_timing": (_I, [_P, _D]),
+    "foto_gn_plan_device": (_I, [_P]),
     "foto_gn_plan_destroy": (None, [_P]),
     "foto_warp": (_I, [_D, _D, _D, _D, _I, _I, _D]),
     "foto_flow_errors": (_I, [_D, _D, _D, _D, _I, _I, _D]),
