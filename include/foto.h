@@ -146,6 +146,13 @@ int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny
 /* RCCL unique id for foto_bb_opts.nccl_id (call on rank 0, broadcast 128 bytes). */
 int foto_nccl_unique_id(void* out128);
 
+/* Test entry: the orthonormal DCT-II (inverse = 0) or DCT-III (inverse = 1) along the middle
+ * axis of a C-order [outer][n][inner] array, as scipy.fft.dct(x, type=2|3, norm="ortho",
+ * axis=1) -- the transform pair that diagonalises lap1d (operators.py:33-48) in the spectral
+ * CG.  path 0: the FFT kernels when n has a plan, else the MFMA GEMM kernels; 1: FFT only
+ * (error without a plan); 2: GEMM only.                                            */
+int foto_dct(const double* in, int outer, int n, int inner, int inverse, int path, double* out);
+
 /* ------------------------------------------------------------------ GN baseline
  * classical.GLLOpticalFlow (classical.py:25-130).                                 */
 /* assemble(f1, f2).A @ x and .b (classical.py:68-111)                             */

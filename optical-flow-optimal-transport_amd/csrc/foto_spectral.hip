@@ -739,6 +739,92 @@ __device__ __forceinline__ void fft_stage2(double* L) {
     }
 }
 
+// Stage 2 for a prime row length P too long for an in-register codelet (~2P live fp64
+// registers: Middlebury's half-lengths 292 = 4 * 73 and 194 = 2 * 97).  The row is
+// transformed in LDS by the symmetric direct DFT: with u_j = z_j + z_{P-j}, v_j = z_j - z_{P-j}
+// (j = 1 .. H, H = (P - 1) / 2), A_k = z_0 + sum_j u_j cos(2 pi jk/P), B_k = sum_j v_j sin(2 pi jk/P):
+//     forward Z_k = A_k - i B_k, Z_{P-k} = A_k + i B_k       (inverse: the conjugate pairing),
+// i.e. ~P real FMA per output instead of 4P.  One task per output pair (k, P - k); the u_j, v_j
+// reads of a row are LDS broadcasts, the roots come from a P-entry table in LDS (CS: cos, sin).
+template <int P>
+struct LdsPrime { static constexpr bool value = P > 32; };
+
+template <int M1, int P, bool INV, int LPB>
+__device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
+    constexpr int LS = FftGeom<M1, P>::LS;
+    constexpr int H = (P - 1) / 2;
+    constexpr int ROWS = LPB * M1;
+    for (int task = threadIdx.x; task < ROWS * H; task += 256) {   // u, v in place
+        const int row = task / H, j = 1 + task - row * H;
+        const int l = row / M1, k1 = row - l * M1;
+        double* Lr = L + l * LS + 2 * (P + 1) * k1;
+        const double ar = Lr[2 * j], ai = Lr[2 * j + 1], br = Lr[2 * (P - j)], bi = Lr[2 * (P - j) + 1];
+        Lr[2 * j] = ar + br;
+        Lr[2 * j + 1] = ai + bi;
+        Lr[2 * (P - j)] = ar - br;
+        Lr[2 * (P - j) + 1] = ai - bi;
+    }
+    __syncthreads();
+    constexpr int T = ROWS * (H + 1);
+    constexpr int RR = (T + 255) / 256;
+    double o[RR][4];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {   // results stay in registers until every read is done
+        const int task = threadIdx.x + 256 * r;
+        o[r][0] = o[r][1] = o[r][2] = o[r][3] = 0.0;
+        if (T % 256 != 0 && task >= T) continue;
+        const int row = task / (H + 1), k = task - row * (H + 1);
+        const int l = row / M1, k1 = row - l * M1;
+        const double* Lr = L + l * LS + 2 * (P + 1) * k1;
+        double Ar = Lr[0], Ai = Lr[1], Br = 0.0, Bi = 0.0;
+        if (k == 0) {
+            for (int j = 1; j <= H; ++j) { Ar += Lr[2 * j]; Ai += Lr[2 * j + 1]; }
+        } else {
+            int q = k;   // j k mod P
+            for (int j = 1; j <= H; ++j) {
+                const double c = CS[2 * q], sn = CS[2 * q + 1];
+                Ar = fma(Lr[2 * j], c, Ar);
+                Ai = fma(Lr[2 * j + 1], c, Ai);
+                Br = fma(Lr[2 * (P - j)], sn, Br);
+                Bi = fma(Lr[2 * (P - j) + 1], sn, Bi);
+                q += k;
+                q = q >= P ? q - P : q;
+            }
+        }
+        o[r][0] = Ar; o[r][1] = Ai; o[r][2] = Br; o[r][3] = Bi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        const int task = threadIdx.x + 256 * r;
+        if (T % 256 != 0 && task >= T) continue;
+        const int row = task / (H + 1), k = task - row * (H + 1);
+        const int l = row / M1, k1 = row - l * M1;
+        double* Lr = L + l * LS + 2 * (P + 1) * k1;
+        const double Ar = o[r][0], Ai = o[r][1], Br = o[r][2], Bi = o[r][3];
+        if (k == 0) {
+            Lr[0] = Ar;
+            Lr[1] = Ai;
+        } else {
+            // A - i B = (Ar + Bi, Ai - Br);  A + i B = (Ar - Bi, Ai + Br)
+            const int kf = INV ? P - k : k, kb = INV ? k : P - k;
+            Lr[2 * kf] = Ar + Bi;
+            Lr[2 * kf + 1] = Ai - Br;
+            Lr[2 * kb] = Ar - Bi;
+            Lr[2 * kb + 1] = Ai + Br;
+        }
+    }
+}
+
+// the stage-2 variant for row length M2, and the LDS root table it needs (doubles)
+template <int M1, int M2, bool INV, int LPB>
+__device__ __forceinline__ void fft_stage2_any(double* L, const double* CS) {
+    if constexpr (LdsPrime<M2>::value) fft_stage2_prime<M1, M2, INV, LPB>(L, CS);
+    else fft_stage2<M1, M2, INV, LPB>(L);
+}
+template <int M2>
+constexpr int fft_cs_len() { return LdsPrime<M2>::value ? 2 * M2 : 2; }
+
 template <int M1, int M2>
 __device__ __forceinline__ int fft_pos(int k) { return (M2 + 1) * (k % M1) + k / M1; }   // where Z_k lands
 
@@ -777,6 +863,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
     using G = FftGeom<M1, M2>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
+    __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
 #if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
 #else
@@ -784,6 +871,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
 #endif
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
+    if constexpr (LdsPrime<M2>::value)
+        for (int p = tid; p < 2 * M2; p += 256) CS[p] = tab[6 * M + 6 + p];
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
@@ -816,7 +905,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
     __syncthreads();
     fft_stage1<M1, M2, false, LPB>(L, TW);
     __syncthreads();
-    fft_stage2<M1, M2, false, LPB>(L);
+    fft_stage2_any<M1, M2, false, LPB>(L, CS);
     __syncthreads();
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
@@ -851,6 +940,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     using G = FftGeom<M1, M2>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
+    __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
 #if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
 #else
@@ -858,6 +948,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
 #endif
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
+    if constexpr (LdsPrime<M2>::value)
+        for (int p = tid; p < 2 * M2; p += 256) CS[p] = tab[6 * M + 6 + p];
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
@@ -920,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     __syncthreads();
     fft_stage1<M1, M2, true, LPB>(L, TW);
     __syncthreads();
-    fft_stage2<M1, M2, true, LPB>(L);
+    fft_stage2_any<M1, M2, true, LPB>(L, CS);
     __syncthreads();
     constexpr double iM = 1.0 / M;
     using RS = FftRounds<LPB * N>;
@@ -939,7 +1031,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
 
 // supported line lengths N = 2 M1 M2 (others use the GEMM kernels)
 #define FOTO_FFT_SIZES(X) X(8, 2, 2) X(16, 2, 4) X(32, 4, 4) X(64, 4, 8) X(128, 8, 8) X(256, 8, 16) \
-    X(480, 15, 16) X(512, 16, 16) X(640, 16, 20) X(1024, 16, 32)
+    X(146, 1, 73) X(194, 1, 97) X(380, 10, 19) X(388, 2, 97) X(420, 14, 15) X(480, 15, 16) X(512, 16, 16) X(584, 4, 73) X(640, 16, 20)    \
+    X(1024, 16, 32)
 
 static bool fft_factors(int n, int* m1, int* m2) {
 #define FOTO_FFT_CASE(NN, A, B) if (n == NN) { *m1 = A; *m2 = B; return true; }
@@ -967,6 +1060,12 @@ static std::vector<double> fft_table(int n) {
     }
     t.push_back((double)sqrtl(1.0L / n));
     t.push_back((double)sqrtl(2.0L / n));
+    int m1 = 0, m2 = 0;
+    if (fft_factors(n, &m1, &m2) && m2 > 32)   // LdsPrime rows: cos, sin of 2 pi q / m2 (at 6 M + 6)
+        for (int q = 0; q < m2; ++q) {
+            t.push_back((double)cosl(2.0L * pi * q / m2));
+            t.push_back((double)sinl(2.0L * pi * q / m2));
+        }
     return t;
 }
 
@@ -2797,3 +2896,55 @@ int SpectralPlan::y0() const { return ((SpecImpl*)impl)->y0; }
 int SpectralPlan::nyl() const { return ((SpecImpl*)impl)->nyl; }
 
 }  // namespace foto
+
+// ============================================================================ C ABI: one DCT axis (test entry)
+
+extern "C" int foto_dct(const double* in, int outer, int n, int inner, int inverse, int path, double* out) {
+    using namespace foto;
+    if (!in || !out || outer < 1 || n < 2 || inner < 1 || path < 0 || path > 2) {
+        set_error("foto_dct: bad arguments");
+        return FOTO_ERR_ARG;
+    }
+    const size_t tot = (size_t)outer * n * inner;
+    hipStream_t s = nullptr;
+    FOTO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void*> bufs;
+    auto dev = [&](size_t nd, double** p) -> int {
+        FOTO_HIP_CHECK(hipMalloc((void**)p, std::max<size_t>(nd, 1) * 8));
+        bufs.push_back(*p);
+        return 0;
+    };
+    auto body = [&]() -> int {
+        double *din, *dout, *dtab = nullptr, *dC;
+        FOTO_TRY(dev(tot, &din));
+        FOTO_TRY(dev(tot, &dout));
+        FOTO_HIP_CHECK(hipMemcpyAsync(din, in, tot * 8, hipMemcpyHostToDevice, s));
+        int m1, m2;
+        hipError_t e = hipErrorNotSupported;
+        if (path != 2 && fft_factors(n, &m1, &m2)) {
+            const std::vector<double> t = fft_table(n);
+            FOTO_TRY(dev(t.size(), &dtab));
+            FOTO_HIP_CHECK(hipMemcpyAsync(dtab, t.data(), t.size() * 8, hipMemcpyHostToDevice, s));
+            FOTO_HIP_CHECK(hipStreamSynchronize(s));
+            e = dct_fft_axis(outer, n, inner, inverse != 0, dtab, din, dout, s);
+        }
+        if (e == hipErrorNotSupported) {
+            if (path == 1) { set_error("foto_dct: no FFT plan for n = %d", n); return FOTO_ERR_ARG; }
+            std::vector<double> C, CT, mu;
+            dct_matrix(n, C, CT, mu);
+            FOTO_TRY(dev(C.size(), &dC));
+            FOTO_HIP_CHECK(hipMemcpyAsync(dC, inverse ? CT.data() : C.data(), C.size() * 8, hipMemcpyHostToDevice, s));
+            FOTO_HIP_CHECK(hipStreamSynchronize(s));
+            e = dct_axis(outer, n, inner, dC, din, dout, s);
+        }
+        FOTO_HIP_CHECK(e);
+        FOTO_HIP_CHECK(hipMemcpyAsync(out, dout, tot * 8, hipMemcpyDeviceToHost, s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        return 0;
+    };
+    const int rc = body();
+    (void)hipStreamSynchronize(s);
+    for (void* p : bufs) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return rc;
+}

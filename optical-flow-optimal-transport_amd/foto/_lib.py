@@ -93,6 +93,7 @@ SIGNATURES = {
     "foto_bb_destroy": (None, [_P]),
     "foto_bb_solve": (_I, [_D, _D, _I, _I, _I, _Dbl, _Dbl, _Dbl, _I, ITER_CB, _P, _D, _D, _D]),
     "foto_nccl_unique_id": (_I, [_P]),
+    "foto_dct": (_I, [_D, _I, _I, _I, _I, _I, _D]),
     "foto_gn_apply": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _D, _D]),
     "foto_gn_rhs": (_I, [_D, _D, _I, _I, _D]),
     "foto_gn_solve": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _Dbl, _I, _D, _D, _D, ctypes.POINTER(_I)]),

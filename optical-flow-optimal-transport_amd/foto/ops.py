@@ -105,3 +105,14 @@ def _bc(bc):
     if bc not in ("N", "D"):
         raise NotImplementedError("These boundary conditions are not implemented")
     return bc.encode()
+
+
+def dct(x, axis_len, inner=1, inverse=False, path=0):
+    """Orthonormal DCT-II (DCT-III if inverse) along the middle axis of a C-order
+    [outer][axis_len][inner] array on the GPU (foto_dct; path 0 auto, 1 FFT, 2 GEMM)."""
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64)).reshape(-1)
+    outer = a.size // (axis_len * inner)
+    assert outer * axis_len * inner == a.size
+    out = np.empty_like(a)
+    check(lib().foto_dct(dptr(a), outer, axis_len, inner, int(bool(inverse)), int(path), dptr(out)))
+    return out
