@@ -740,12 +740,17 @@ __device__ __forceinline__ void fft_stage2(double* L) {
 }
 
 // Stage 2 for a prime row length P too long for an in-register codelet (~2P live fp64
-// registers: Middlebury's half-lengths 292 = 4 * 73 and 194 = 2 * 97).  The row is
-// transformed in LDS by the symmetric direct DFT: with u_j = z_j + z_{P-j}, v_j = z_j - z_{P-j}
-// (j = 1 .. H, H = (P - 1) / 2), A_k = z_0 + sum_j u_j cos(2 pi jk/P), B_k = sum_j v_j sin(2 pi jk/P):
-//     forward Z_k = A_k - i B_k, Z_{P-k} = A_k + i B_k       (inverse: the conjugate pairing),
-// i.e. ~P real FMA per output instead of 4P.  One task per output pair (k, P - k); the u_j, v_j
-// reads of a row are LDS broadcasts, the roots come from a P-entry table in LDS (CS: cos, sin).
+// registers: Middlebury's half-lengths 292 = 4 * 73 and 194 = 2 * 97).  Symmetric direct DFT:
+// with u_j = z_j + z_{P-j}, v_j = z_j - z_{P-j} (j = 1 .. H, H = (P - 1) / 2),
+//     A_k = z_0 + sum_j u_j cos(2 pi jk/P),   B_k = sum_j v_j sin(2 pi jk/P),   k = 0 .. H,
+//     forward Z_k = A_k - i B_k, Z_{P-k} = A_k + i B_k       (inverse: the conjugate pairing).
+// For all ROWS rows of the block the two sums are real GEMMs, (2 ROWS x H) (H x (H + 1)),
+// run on the f64 MFMA (v_mfma_f64_16x16x4_f64): an M tile is 8 complex rows (tile rows 0-7
+// their real parts, 8-15 their imaginary parts, so a lane's four results are the real and
+// imaginary parts of two rows in one output column), K = H (a multiple of 4), N = H + 1
+// padded to 16.  The B operands (cos, sin of 2 pi q / P) come from the P-entry root table CS in
+// LDS, one 16-B read per k-step and N tile for both GEMMs.  (A direct per-output loop read
+// ~48 B of LDS per multiply-add and was LDS-bound: 70-95 us per axis pass at 584x388x32.)
 template <int P>
 struct LdsPrime { static constexpr bool value = P > 32; };
 
@@ -754,6 +759,8 @@ __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
     constexpr int LS = FftGeom<M1, P>::LS;
     constexpr int H = (P - 1) / 2;
     constexpr int ROWS = LPB * M1;
+    constexpr int KS = H / 4, NTL = (H + 1 + 15) / 16, MT = ROWS / 8;
+    static_assert(H % 4 == 0 && ROWS % 8 == 0, "prime stage: K steps of 4, M tiles of 8 rows");
     for (int task = threadIdx.x; task < ROWS * H; task += 256) {   // u, v in place
         const int row = task / H, j = 1 + task - row * H;
         const int l = row / M1, k1 = row - l * M1;
@@ -765,53 +772,74 @@ __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
         Lr[2 * (P - j) + 1] = ai - bi;
     }
     __syncthreads();
-    constexpr int T = ROWS * (H + 1);
-    constexpr int RR = (T + 255) / 256;
-    double o[RR][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int am = lane & 15, ak = lane >> 4;   // A operand: row am, k ak of the step
+    constexpr int MTW = (MT + 3) / 4;           // M tiles per wave
+    dbl4 dc[MTW][NTL], ds[MTW][NTL];
+    double z0r[MTW][2], z0i[MTW][2];
 #pragma unroll
-    for (int r = 0; r < RR; ++r) {   // results stay in registers until every read is done
-        const int task = threadIdx.x + 256 * r;
-        o[r][0] = o[r][1] = o[r][2] = o[r][3] = 0.0;
-        if (T % 256 != 0 && task >= T) continue;
-        const int row = task / (H + 1), k = task - row * (H + 1);
-        const int l = row / M1, k1 = row - l * M1;
-        const double* Lr = L + l * LS + 2 * (P + 1) * k1;
-        double Ar = Lr[0], Ai = Lr[1], Br = 0.0, Bi = 0.0;
-        if (k == 0) {
-            for (int j = 1; j <= H; ++j) { Ar += Lr[2 * j]; Ai += Lr[2 * j + 1]; }
-        } else {
-            int q = k;   // j k mod P
-            for (int j = 1; j <= H; ++j) {
-                const double c = CS[2 * q], sn = CS[2 * q + 1];
-                Ar = fma(Lr[2 * j], c, Ar);
-                Ai = fma(Lr[2 * j + 1], c, Ai);
-                Br = fma(Lr[2 * (P - j)], sn, Br);
-                Bi = fma(Lr[2 * (P - j) + 1], sn, Bi);
-                q += k;
-                q = q >= P ? q - P : q;
+    for (int w = 0; w < MTW; ++w) {
+        const int mt = wave + 4 * w;
+        if (MT % 4 != 0 && mt >= MT) continue;
+        // this lane's A row: complex row 8 mt + (am & 7), real (am < 8) or imaginary part
+        const int rowa = 8 * mt + (am & 7);
+        const int offa = (rowa / M1) * LS + 2 * (P + 1) * (rowa % M1) + (am >> 3);
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) { dc[w][t] = dbl4{0.0, 0.0, 0.0, 0.0}; ds[w][t] = dbl4{0.0, 0.0, 0.0, 0.0}; }
+#pragma unroll 3
+        for (int ks = 0; ks < KS; ++ks) {
+            const int j = 4 * ks + ak + 1;
+            const double au = L[offa + 2 * j], av = L[offa + 2 * (P - j)];
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) {
+                const int n = 16 * t + am;   // B operand: k ak, column n
+                double bc = 0.0, bs = 0.0;
+                if (n <= H) {
+                    const int q = (j * n) % P;
+                    bc = CS[2 * q];
+                    bs = CS[2 * q + 1];
+                }
+                dc[w][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bc, dc[w][t], 0, 0, 0);
+                ds[w][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bs, ds[w][t], 0, 0, 0);
             }
         }
-        o[r][0] = Ar; o[r][1] = Ai; o[r][2] = Br; o[r][3] = Bi;
+        // D rows of this lane: (lane >> 4) + 4 reg -> complex rows g, g + 4 of the tile (reg 0, 1
+        // real, reg 2, 3 imaginary); their z_0
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = 8 * mt + (lane >> 4) + 4 * h;
+            const double* Lr = L + (row / M1) * LS + 2 * (P + 1) * (row % M1);
+            z0r[w][h] = Lr[0];
+            z0i[w][h] = Lr[1];
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < RR; ++r) {
-        const int task = threadIdx.x + 256 * r;
-        if (T % 256 != 0 && task >= T) continue;
-        const int row = task / (H + 1), k = task - row * (H + 1);
-        const int l = row / M1, k1 = row - l * M1;
-        double* Lr = L + l * LS + 2 * (P + 1) * k1;
-        const double Ar = o[r][0], Ai = o[r][1], Br = o[r][2], Bi = o[r][3];
-        if (k == 0) {
-            Lr[0] = Ar;
-            Lr[1] = Ai;
-        } else {
-            // A - i B = (Ar + Bi, Ai - Br);  A + i B = (Ar - Bi, Ai + Br)
-            const int kf = INV ? P - k : k, kb = INV ? k : P - k;
-            Lr[2 * kf] = Ar + Bi;
-            Lr[2 * kf + 1] = Ai - Br;
-            Lr[2 * kb] = Ar - Bi;
-            Lr[2 * kb + 1] = Ai + Br;
+    for (int w = 0; w < MTW; ++w) {
+        const int mt = wave + 4 * w;
+        if (MT % 4 != 0 && mt >= MT) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = 8 * mt + (lane >> 4) + 4 * h;
+            double* Lr = L + (row / M1) * LS + 2 * (P + 1) * (row % M1);
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) {
+                const int k = 16 * t + (lane & 15);
+                if (k > H) continue;
+                const double Ar = z0r[w][h] + dc[w][t][h], Ai = z0i[w][h] + dc[w][t][2 + h];
+                const double Br = ds[w][t][h], Bi = ds[w][t][2 + h];
+                if (k == 0) {
+                    Lr[0] = Ar;
+                    Lr[1] = Ai;
+                } else {
+                    // A - i B = (Ar + Bi, Ai - Br);  A + i B = (Ar - Bi, Ai + Br)
+                    const int kf = INV ? P - k : k, kb = INV ? k : P - k;
+                    Lr[2 * kf] = Ar + Bi;
+                    Lr[2 * kf + 1] = Ai - Br;
+                    Lr[2 * kb] = Ar - Bi;
+                    Lr[2 * kb + 1] = Ai + Br;
+                }
+            }
         }
     }
 }
