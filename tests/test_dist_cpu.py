@@ -9,6 +9,13 @@ the single-process oracle: identical CG counts, same crit / phi / flow to 1e-9. 
 rendezvous used by bench.py (RCCL unique-id broadcast, barrier, max-over-ranks timing) is
 exercised as well.  The GPU-side counterpart (virtual ranks on one device) is
 tests/test_gpu_parity.py::test_bb_virtual_ranks_match_single.
+
+The default sharded CG (the spectral s-step CG, csrc/foto_bb.cpp cg_solve_spectral_sharded)
+is restated too: x/y DCTs of the own time planes, the slab -> row-box all-to-all with the
+library's packing and region arithmetic (k_spec_pack, alltoall_spec), the t-DCT on the box,
+s-step passes whose 48 Chebyshev moments are all-gathered and summed in rank order so that
+every rank plans identically (the numpy planning rule of tests/test_sstep_plan.py), and the
+way back.  It must reproduce scipy's CG (the oracle) on the same right-hand side.
 """
 import os
 import socket
@@ -284,6 +291,188 @@ def test_bench_rendezvous_gloo():
     ids = {r[1] for r in res}
     assert len(ids) == 1 and len(next(iter(ids))) == 128
     assert all(r[2] == 0.5 + (W - 1) for r in res)
+
+
+# ---------------------------------------------------------------- spectral s-step CG over slabs
+
+def _owner(n, W, i):
+    """csrc/foto_spectral.hip split_owner."""
+    base, extra = divmod(n, W)
+    big = extra * (base + 1)
+    return i // (base + 1) if i < big else extra + (i - big) // base
+
+
+def _exchange(sends, recvs):
+    """the grouped ncclSend / ncclRecv of foto_bb.cpp as isend / irecv pairs (gloo)."""
+    reqs = [dist.isend(torch.from_numpy(np.ascontiguousarray(buf)), peer) for peer, buf in sends]
+    outs = []
+    for peer, n in recvs:
+        t = torch.zeros(n, dtype=torch.float64)
+        reqs.append(dist.irecv(t, peer))
+        outs.append((peer, t))
+    for r in reqs:
+        r.wait()
+    return {peer: t.numpy() for peer, t in outs}
+
+
+def _regions(Nt, Ny, Nx, W, a, b, forward):
+    """foto_bb.cpp alltoall_spec: what rank a sends to rank b (offsets and count, doubles)."""
+    ta, na = split_planes(Nt, W, a)
+    tb, nb = split_planes(Nt, W, b)
+    ya, nya = split_planes(Ny, W, a)
+    yb, nyb = split_planes(Ny, W, b)
+    if forward:
+        return na * Nx * yb, ta * nyb * Nx, na * nyb * Nx
+    return tb * nya * Nx, nb * Nx * ya, nb * nya * Nx
+
+
+def _alltoall(S, sbuf, rsize, forward):
+    W, g = S.W, S.rank
+    rbuf = np.zeros(rsize)
+    sends, recvs = [], []
+    for h in range(W):
+        so, ro, n = _regions(S.Nt, S.Ny, S.Nx, W, g, h, forward)
+        if h == g:
+            if n:
+                rbuf[ro:ro + n] = sbuf[so:so + n]
+            continue
+        if n:
+            sends.append((h, sbuf[so:so + n]))
+        so2, ro2, n2 = _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward)
+        if n2:
+            recvs.append((h, n2))
+    got = _exchange(sends, recvs)
+    for h, buf in got.items():
+        _, ro2, n2 = _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward)
+        rbuf[ro2:ro2 + n2] = buf
+    return rbuf
+
+
+def _pack(S, planes, unpack_from=None):
+    """k_spec_pack: own planes [tl][y][x] <-> staging [h][tl][y - y0_h][x]."""
+    Ny, Nx, W, nloc = S.Ny, S.Nx, S.W, S.nloc
+    stage = np.zeros(nloc * Ny * Nx) if unpack_from is None else unpack_from
+    out = np.zeros((nloc, Ny, Nx))
+    for y in range(Ny):
+        h = _owner(Ny, W, y)
+        y0h, nyh = split_planes(Ny, W, h)
+        for tl in range(nloc):
+            j = nloc * Nx * y0h + (tl * nyh + (y - y0h)) * Nx
+            if unpack_from is None:
+                stage[j:j + Nx] = planes[tl, y]
+            else:
+                out[tl, y] = stage[j:j + Nx]
+    return stage if unpack_from is None else out
+
+
+def sharded_spectral_cg(S, F, r, eps, rtol=1e-6, maxiter=1000):
+    """Returns (phi on the own planes, iterations, the per-pass step counts and alphas)."""
+    import math
+    import scipy.fft as sfft
+    import test_sstep_plan as SP
+    Nt, Ny, Nx, W = S.Nt, S.Ny, S.Nx, S.W
+    y0, nyl = split_planes(Ny, W, S.rank)
+    # x, y DCTs of the own planes, slab -> box, t-DCT
+    Fh = sfft.dct(sfft.dct(F, type=2, norm="ortho", axis=2), type=2, norm="ortho", axis=1)
+    box = _alltoall(S, _pack(S, Fh), Nt * nyl * Nx, True).reshape(Nt, nyl, Nx)
+    bh = sfft.dct(box, type=2, norm="ortho", axis=0).ravel()
+    mu = lambda n: 2 - 2 * np.cos(np.pi * np.arange(n) / n)  # noqa: E731
+    lam = (r * eps + r * (mu(Nt)[:, None, None] + mu(Ny)[None, y0:y0 + nyl, None]
+                          + mu(Nx)[None, None, :])).ravel()
+    lmin = r * eps
+    lmax = r * eps + r * (mu(Nt).max() + mu(Ny).max() + mu(Nx).max())
+    c0, c1 = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
+
+    def moments(rr, q):
+        x = (lam - c0) / c1
+        T = np.empty((SP.NMOM, lam.size))
+        T[0], T[1] = 1.0, x
+        for m in range(2, SP.NMOM):
+            T[m] = 2 * x * T[m - 1] - T[m - 2]
+        loc = np.concatenate([SP._moments(T, rr * rr), SP._moments(T, rr * q), SP._moments(T, q * q)])
+        t = torch.from_numpy(loc)
+        parts = [torch.zeros_like(t) for _ in range(W)]
+        dist.all_gather(parts, t)   # foto_bb.cpp: one NACC-double all-gather per pass
+        tot = np.zeros_like(loc)
+        for g in range(W):          # summed in rank order on every rank
+            tot = tot + parts[g].numpy()
+        return tot[:SP.NMOM], tot[SP.NMOM:2 * SP.NMOM], tot[2 * SP.NMOM:]
+
+    rr, q = bh.copy(), np.zeros_like(bh)
+    Mrr, Mrq, Mqq = moments(rr, q)
+    atol = max(0.0, rtol * math.sqrt(Mrr[0]))
+    k, rho_prev, conv, log = 0, 0.0, False, []
+    while k < maxiter:
+        al, be, conv, rho_prev, proj = SP._plan(Mrr, Mrq, Mqq, k, rho_prev, atol, c0, c1, maxiter)
+        log.append(tuple(al))
+        ms = SP._moment_stats(Mrr, c0, c1)
+        if proj is not None:
+            c0, c1 = SP._interval(*proj, c0, c1, lmin, lmax)
+        elif ms is not None:
+            c0, c1 = SP._interval(*ms, c0, c1, lmin, lmax)
+        for a, bt in zip(al, be):
+            p = rr.copy() if k == 0 else bt * q + rr
+            rr = rr - a * (lam * p)
+            q = p
+            k += 1
+        if conv or not al:
+            break
+        Mrr, Mrq, Mqq = moments(rr, q)
+    # x^ = (b^ - r^) / lam, inverse t-DCT, box -> slab, inverse y, x
+    xt = sfft.dct(((bh - rr) / lam).reshape(Nt, nyl, Nx), type=3, norm="ortho", axis=0)
+    stage = _alltoall(S, xt.ravel(), S.nloc * Ny * Nx, False)
+    phi = _pack(S, None, unpack_from=stage)
+    phi = sfft.dct(sfft.dct(phi, type=3, norm="ortho", axis=1), type=3, norm="ortho", axis=2)
+    return phi, k, log
+
+
+def _spectral_worker(rank, W, port, q, case):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(REPO, "optical-flow-optimal-transport_amd"))
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=W)
+    try:
+        Nt, Ny, Nx, r, eps = case
+        F = np.random.default_rng(7).standard_normal((Nt, Ny, Nx))
+        S = Shard(rank, W, Nt, Ny, Nx)
+        phi, its, log = sharded_spectral_cg(S, F[S.t0:S.t0 + S.nloc], r, eps)
+        parts = [torch.zeros(Nt * Ny * Nx, dtype=torch.float64) for _ in range(W)]
+        mine = torch.zeros(Nt * Ny * Nx, dtype=torch.float64)
+        mine[S.t0 * Ny * Nx:(S.t0 + S.nloc) * Ny * Nx] = torch.from_numpy(phi.ravel())
+        dist.all_gather(parts, mine)
+        q.put((rank, its, log, sum(p.numpy() for p in parts) if rank == 0 else None))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_sharded_spectral_cg_matches_oracle(W):
+    """Uneven splits on both axes (Nt = 7, Ny = 10 over 2 and 3 ranks): every rank plans the
+    same steps, and the gathered phi is scipy's CG solution (iterations +-1, 5e-8 of max|x|:
+    the bar of the single-GPU spectral CG)."""
+    sys.path.insert(0, REPO)
+    from oracle import foto_oracle as O
+    case = (7, 10, 12, 1.0, 1e-2)
+    Nt, Ny, Nx, r, eps = case
+    ctx = mp.get_context("spawn")
+    qu = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spectral_worker, args=(g, W, port, qu, case)) for g in range(W)]
+    for p in procs:
+        p.start()
+    res = sorted([qu.get(timeout=300) for _ in range(W)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len({t[1] for t in res}) == 1 and len({tuple(t[2]) for t in res}) == 1   # identical plans
+    phi = res[0][3]
+    F = np.random.default_rng(7).standard_normal((Nt, Ny, Nx)).ravel()
+    A = O.assemble_A(r, eps, Nt, Ny, Nx)
+    x, info, its = O.cg(A.dot, F, rtol=1e-6, maxiter=1000)
+    assert info == 0 and abs(res[0][1] - its) <= 1
+    np.testing.assert_allclose(phi, x, rtol=0, atol=5e-8 * np.abs(x).max())
+    assert len(res[0][2]) < its / 3   # s-step: far fewer passes (all-gathers) than iterations
 
 
 def test_split_planes_matches_library_rule():
