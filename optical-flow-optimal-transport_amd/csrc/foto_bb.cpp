@@ -144,8 +144,51 @@ struct foto_bb_ctx {
 namespace foto {
 
 // ----------------------------------------------------------------------------- communication
-// Virtual ranks share one stream, so plain device copies keep everything ordered.
+// Every exchange between shards is a list of point-to-point transfers, built by the same
+// code on every rank and for every transport; only its execution differs:
+//   virtual ranks (one process, all shards on one device and stream): one device copy per
+//   transfer, in list order;
+//   RCCL (one shard per process): in one group, ncclSend for each transfer from this rank and
+//   ncclRecv for each transfer to it (pairs match in list order, which is the same on every
+//   rank); a transfer to itself is a device copy.
+// Offsets are in doubles from the pointer a picker returns for the shard (negative: the halo
+// plane below).  The virtual-rank GPU tests therefore run the very lists RCCL executes.
+struct Xfer {
+    int src, dst;
+    int64_t soff, doff, n;
+};
 
+template <class SrcPick, class DstPick>
+static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, DstPick dp) {
+    if (!c->rccl) {
+        for (const Xfer& x : xs)
+            FOTO_HIP_CHECK(hipMemcpyAsync(dp(*c->sh[x.dst]) + x.doff, sp(*c->sh[x.src]) + x.soff,
+                                          (size_t)x.n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
+        return 0;
+    }
+    Shard& s = *c->sh[0];
+    const int me = s.rank;
+    bool any = false;
+    for (const Xfer& x : xs) any = any || ((x.src == me) != (x.dst == me));
+    if (any) {
+        FOTO_NCCL_CHECK(ncclGroupStart());
+        for (const Xfer& x : xs) {
+            if (x.src == me && x.dst != me)
+                FOTO_NCCL_CHECK(ncclSend(sp(s) + x.soff, (size_t)x.n, ncclDouble, x.dst, c->nc, c->s));
+            if (x.dst == me && x.src != me)
+                FOTO_NCCL_CHECK(ncclRecv(dp(s) + x.doff, (size_t)x.n, ncclDouble, x.src, c->nc, c->s));
+        }
+        FOTO_NCCL_CHECK(ncclGroupEnd());
+    }
+    for (const Xfer& x : xs)
+        if (x.src == me && x.dst == me)
+            FOTO_HIP_CHECK(hipMemcpyAsync(dp(s) + x.doff, sp(s) + x.soff, (size_t)x.n * sizeof(double),
+                                          hipMemcpyDeviceToDevice, c->s));
+    return 0;
+}
+
+// each rank's `cnt` doubles at slot [rank] of the picked array to every rank's same slot
+// (RCCL: one ncclAllGather, in place; virtual ranks: the equivalent copies)
 template <class Pick>
 static int allgather(foto_bb_ctx* c, Pick pick, int cnt) {
     if (c->W == 1) return 0;
@@ -155,46 +198,21 @@ static int allgather(foto_bb_ctx* c, Pick pick, int cnt) {
         FOTO_NCCL_CHECK(ncclAllGather(base + (size_t)s.rank * cnt, base, cnt, ncclDouble, c->nc, c->s));
         return 0;
     }
-    for (auto& a : c->sh)
-        for (auto& b : c->sh)
-            if (a.get() != b.get())
-                FOTO_HIP_CHECK(hipMemcpyAsync(pick(*a) + (size_t)b->rank * cnt, pick(*b) + (size_t)b->rank * cnt,
-                                              cnt * sizeof(double), hipMemcpyDeviceToDevice, c->s));
-    return 0;
+    std::vector<Xfer> xs;
+    for (int g = 0; g < c->W; ++g)
+        for (int h = 0; h < c->W; ++h)
+            if (g != h) xs.push_back({g, h, (int64_t)g * cnt, (int64_t)g * cnt, cnt});
+    return exchange(c, xs, pick, pick);
 }
 
 // halo planes of a halo-padded field: plane -1 <- previous rank's last plane, plane nloc <-
-// next rank's first plane.
+// next rank's first plane
+static std::vector<Xfer> halo_xfers(const foto_bb_ctx* c);
+
 template <class Pick>
 static int halo(foto_bb_ctx* c, Pick pick) {
     if (c->W == 1) return 0;
-    if (c->rccl) {
-        Shard& s = *c->sh[0];
-        double* a = pick(s);
-        const size_t n = (size_t)s.g.nxy;
-        FOTO_NCCL_CHECK(ncclGroupStart());
-        if (s.rank > 0) {
-            FOTO_NCCL_CHECK(ncclSend(a, n, ncclDouble, s.rank - 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclRecv(a - n, n, ncclDouble, s.rank - 1, c->nc, c->s));
-        }
-        if (s.rank < c->W - 1) {
-            FOTO_NCCL_CHECK(ncclSend(a + (size_t)(s.g.nloc - 1) * n, n, ncclDouble, s.rank + 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclRecv(a + (size_t)s.g.nloc * n, n, ncclDouble, s.rank + 1, c->nc, c->s));
-        }
-        FOTO_NCCL_CHECK(ncclGroupEnd());
-        return 0;
-    }
-    for (size_t j = 0; j + 1 < c->sh.size(); ++j) {
-        Shard& lo = *c->sh[j];
-        Shard& hi = *c->sh[j + 1];
-        const size_t n = (size_t)lo.g.nxy;
-        double* a = pick(lo);
-        double* b = pick(hi);
-        FOTO_HIP_CHECK(hipMemcpyAsync(a + (size_t)lo.g.nloc * n, b, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
-        FOTO_HIP_CHECK(hipMemcpyAsync(b - n, a + (size_t)(lo.g.nloc - 1) * n, n * sizeof(double),
-                                      hipMemcpyDeviceToDevice, c->s));
-    }
-    return 0;
+    return exchange(c, halo_xfers(c), pick, pick);
 }
 
 // ----------------------------------------------------------------------------- context setup
@@ -261,6 +279,18 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     }
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     return 0;
+}
+
+static std::vector<Xfer> halo_xfers(const foto_bb_ctx* c) {
+    std::vector<Xfer> xs;
+    const int64_t nxy = (int64_t)c->Nx * c->Ny;
+    for (int j = 0; j + 1 < c->W; ++j) {
+        int t0, nl;
+        split_planes(c->Nt, c->W, j, &t0, &nl);
+        xs.push_back({j, j + 1, (int64_t)(nl - 1) * nxy, -nxy, nxy});   // up: last plane -> halo below
+        xs.push_back({j + 1, j, 0, (int64_t)nl * nxy, nxy});             // down: first plane -> halo above
+    }
+    return xs;
 }
 
 // ----------------------------------------------------------------------------- CG driver
@@ -331,34 +361,14 @@ static int alltoall_spec(foto_bb_ctx* c, bool forward) {
     };
     auto sbuf = [&](Shard& s) { return forward ? s.spec->stage() : s.spec->box_out(); };
     auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.spec->stage(); };
-    if (!c->rccl) {
-        for (auto& a : c->sh)
-            for (auto& b : c->sh) {
-                int64_t so, ro, n;
-                region(a->rank, b->rank, &so, &ro, &n);
-                if (n > 0)
-                    FOTO_HIP_CHECK(hipMemcpyAsync(rbuf(*b) + ro, sbuf(*a) + so, n * sizeof(double),
-                                                  hipMemcpyDeviceToDevice, c->s));
-            }
-        return 0;
-    }
-    Shard& s = *c->sh[0];
-    const int g = s.rank;
-    FOTO_NCCL_CHECK(ncclGroupStart());
-    for (int h = 0; h < W; ++h) {
-        if (h == g) continue;
-        int64_t so, ro, n;
-        region(g, h, &so, &ro, &n);   // what g sends to h
-        if (n > 0) FOTO_NCCL_CHECK(ncclSend(sbuf(s) + so, (size_t)n, ncclDouble, h, c->nc, c->s));
-        region(h, g, &so, &ro, &n);   // what g receives from h
-        if (n > 0) FOTO_NCCL_CHECK(ncclRecv(rbuf(s) + ro, (size_t)n, ncclDouble, h, c->nc, c->s));
-    }
-    FOTO_NCCL_CHECK(ncclGroupEnd());
-    int64_t so, ro, n;
-    region(g, g, &so, &ro, &n);
-    if (n > 0)
-        FOTO_HIP_CHECK(hipMemcpyAsync(rbuf(s) + ro, sbuf(s) + so, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
-    return 0;
+    std::vector<Xfer> xs;
+    for (int a = 0; a < W; ++a)
+        for (int b = 0; b < W; ++b) {
+            int64_t so, ro, n;
+            region(a, b, &so, &ro, &n);
+            if (n > 0) xs.push_back({a, b, so, ro, n});
+        }
+    return exchange(c, xs, sbuf, rbuf);
 }
 
 // Spectral s-step CG over time-slab shards: x/y DCTs on the own planes, all-to-all to
@@ -588,63 +598,38 @@ static int flow(foto_bb_ctx* c, double* u, double* v, double* m) {
     }
     const int W = c->W;
     FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
-    if (c->rccl) {
-        Shard& s = *c->sh[0];
-        const size_t n = (size_t)s.g.nxy;
-        if (s.rank > 0) {
-            FOTO_NCCL_CHECK(ncclGroupStart());
-            FOTO_NCCL_CHECK(ncclRecv(s.px, n, ncclDouble, s.rank - 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclRecv(s.py, n, ncclDouble, s.rank - 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclGroupEnd());
+    // Trajectories relay rank to rank: rank j runs the steps of its planes, then its
+    // positions travel to rank j + 1; the last rank finishes (u, v, m) and delivers them to
+    // rank 0.  The same transfer lists for both transports (exchange()).
+    const int64_t nxy = (int64_t)c->Nx * c->Ny;
+    auto local = [&](int rank) -> Shard* {
+        for (auto& sp : c->sh)
+            if (sp->rank == rank) return sp.get();
+        return nullptr;
+    };
+    for (int j = 0; j < W; ++j) {
+        if (Shard* s = local(j)) {
+            const int n_lo = s->g.t0, n_hi = std::min(s->g.t0 + s->g.nloc, c->Nt - 1);
+            FOTO_HIP_CHECK(launch_traj(s->g, s->phi, n_lo, std::max(n_lo, n_hi), s->px, s->py, j == 0, c->s));
+            if (j == W - 1) FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s->px, s->py, s->fu, s->fv, s->fm, c->s));
         }
-        const int n_lo = s.g.t0, n_hi = std::min(s.g.t0 + s.g.nloc, c->Nt - 1);
-        FOTO_HIP_CHECK(launch_traj(s.g, s.phi, n_lo, std::max(n_lo, n_hi), s.px, s.py, s.rank == 0, c->s));
-        if (s.rank < W - 1) {
-            FOTO_NCCL_CHECK(ncclGroupStart());
-            FOTO_NCCL_CHECK(ncclSend(s.px, n, ncclDouble, s.rank + 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclSend(s.py, n, ncclDouble, s.rank + 1, c->nc, c->s));
-            FOTO_NCCL_CHECK(ncclGroupEnd());
-        } else {
-            FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s.px, s.py, s.fu, s.fv, s.fm, c->s));
+        if (j + 1 < W) {
+            const std::vector<Xfer> xs = {{j, j + 1, 0, 0, nxy}};
+            FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.px; }, [](Shard& s) { return s.px; }));
+            FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.py; }, [](Shard& s) { return s.py; }));
         }
-        // deliver (u, v, m) to rank 0
-        if (W > 1) {
-            FOTO_NCCL_CHECK(ncclGroupStart());
-            if (s.rank == W - 1) {
-                FOTO_NCCL_CHECK(ncclSend(s.fu, n, ncclDouble, 0, c->nc, c->s));
-                FOTO_NCCL_CHECK(ncclSend(s.fv, n, ncclDouble, 0, c->nc, c->s));
-                FOTO_NCCL_CHECK(ncclSend(s.fm, n, ncclDouble, 0, c->nc, c->s));
-            }
-            if (s.rank == 0) {
-                FOTO_NCCL_CHECK(ncclRecv(s.fu, n, ncclDouble, W - 1, c->nc, c->s));
-                FOTO_NCCL_CHECK(ncclRecv(s.fv, n, ncclDouble, W - 1, c->nc, c->s));
-                FOTO_NCCL_CHECK(ncclRecv(s.fm, n, ncclDouble, W - 1, c->nc, c->s));
-            }
-            FOTO_NCCL_CHECK(ncclGroupEnd());
-        }
-        if (s.rank == 0 && u && v && m) {
-            FOTO_HIP_CHECK(hipMemcpyAsync(u, s.fu, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipMemcpyAsync(v, s.fv, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipMemcpyAsync(m, s.fm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-        }
-    } else {
-        for (size_t j = 0; j < c->sh.size(); ++j) {
-            Shard& s = *c->sh[j];
-            const size_t n = (size_t)s.g.nxy;
-            if (j > 0) {
-                FOTO_HIP_CHECK(hipMemcpyAsync(s.px, c->sh[j - 1]->px, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
-                FOTO_HIP_CHECK(hipMemcpyAsync(s.py, c->sh[j - 1]->py, n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
-            }
-            const int n_lo = s.g.t0, n_hi = std::min(s.g.t0 + s.g.nloc, c->Nt - 1);
-            FOTO_HIP_CHECK(launch_traj(s.g, s.phi, n_lo, std::max(n_lo, n_hi), s.px, s.py, j == 0, c->s));
-        }
-        Shard& s = *c->sh.back();
-        const size_t n = (size_t)s.g.nxy;
-        FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s.px, s.py, s.fu, s.fv, s.fm, c->s));
+    }
+    if (W > 1) {
+        const std::vector<Xfer> xs = {{W - 1, 0, 0, 0, nxy}};
+        FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fu; }, [](Shard& s) { return s.fu; }));
+        FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fv; }, [](Shard& s) { return s.fv; }));
+        FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fm; }, [](Shard& s) { return s.fm; }));
+    }
+    if (Shard* s0 = local(0)) {
         if (u && v && m) {
-            FOTO_HIP_CHECK(hipMemcpyAsync(u, s.fu, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipMemcpyAsync(v, s.fv, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipMemcpyAsync(m, s.fm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(u, s0->fu, nxy * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(v, s0->fv, nxy * sizeof(double), hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipMemcpyAsync(m, s0->fm, nxy * sizeof(double), hipMemcpyDeviceToHost, c->s));
         }
     }
     FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
