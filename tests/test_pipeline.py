@@ -182,6 +182,30 @@ def test_pipeline_gpu_end_to_end(tmp_path):
     assert os.path.getmtime(tmp_path / "results" / "middlebury-1" / "Army" / "foto.flo") == before
 
 
+@pytest.mark.gpu
+def test_pipeline_gpu_vs_reference_cli(gold, tmp_path):
+    """The pipeline's per-sequence run against the reference itself: tests/golden/cli.npz
+    holds the reference main.py's results on a 36x28 PNG pair (make_golden.py, GN with
+    run.sh's alpha / lambda, FOTO with Nt = 4, 8 outer iterations).  The same PNG bytes as a
+    one-sequence dataset through run.py (FOTO parameters forwarded after `--`) give the same
+    .flo to 1e-5 px and the same IE."""
+    d = gold("cli.npz")
+    frames = tmp_path / "frames"
+    (frames / "Pair").mkdir(parents=True)
+    d["png0"].tofile(frames / "Pair" / "frame10.png")
+    d["png1"].tofile(frames / "Pair" / "frame11.png")
+    assert pipeline.main(["run", f"--data={tmp_path / 'nodata'}", f"--results={tmp_path / 'results'}",
+                          f"--dataset=ref={frames}", "--", "--Nt=4", "--max-it=8"]) == 0
+    for algo, key in (("gn", "GN"), ("foto", "foto")):
+        w, h, uu, vv = utils.openFlo(str(tmp_path / "results" / "ref" / "Pair" / f"{algo}.flo"))
+        assert (w, h) == (36, 28)
+        ref = np.frombuffer(d[f"{key}_flo"].tobytes()[12:], dtype=np.float32)
+        np.testing.assert_allclose(np.stack([uu, vv], 1).ravel(), ref, rtol=0, atol=1e-5)
+    rows = {r["algo"]: r for r in json.load(open(tmp_path / "results" / "summary.json")) if r["sequence"] == "Pair"}
+    for algo, key in (("gn", "GN"), ("foto", "foto")):
+        assert abs(float(rows[algo]["IE"]) - float(d[f"{key}_ie"])) < 1e-4
+
+
 def test_worker_argv_round_trip(tmp_path):
     """`--gpus N` re-invokes run.py per GPU; the children must see the parent's options."""
     a = pipeline.parse_args(["run", "--gpus=4", f"--data={tmp_path}/d", "--results=r",
