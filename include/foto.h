@@ -159,8 +159,9 @@ int foto_dct(const double* in, int outer, int n, int inner, int inverse, int pat
 int foto_gn_apply(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   const double* x3, double* y3);
 int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
-/* process(): spsolve replaced by CG preconditioned by a multigrid V-cycle (block-Jacobi
- * smoothing, FOTO_GN_MG=0: plain block-Jacobi PCG) to rtol (default 1e-10).
+/* process(): spsolve replaced by CG preconditioned by one multigrid V-cycle (damped
+ * block-Jacobi smoothing on each level; FOTO_GN_MG=0: the plain 3x3 block-Jacobi PCG) to rtol
+ * (default 1e-10).
  * Returns 0 (converged) or maxiter (not converged), < 0 on error.  Runs on a plan (below)
  * cached per process for the last (w, h, alpha, lambda, rtol, maxiter, device), as FFT
  * libraries cache plans; FOTO_GN_PLAN_CACHE=0 makes and destroys one per call.       */
