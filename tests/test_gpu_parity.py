@@ -192,9 +192,16 @@ def test_bb_solve_c1(gold, mode):
                     stats=st, log=lambda s: None, cg_mode=mode)
     assert len(st["crit"]) == len(d["crit"]) == 46
     assert np.max(np.abs(st["cg_its"] - d["cg_its"])) <= 1
-    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-5, atol=0)
+    print(f"C1 mode {mode}: crit rel {np.max(np.abs(np.array(st['crit']) - d['crit']) / d['crit']):.2e}, "
+          f"flow {max(np.abs(a - b).max() for a, b in ((u, d['u']), (v, d['v']), (m, d['m']))):.2e} px, "
+          f"cg its diff {np.abs(st['cg_its'] - d['cg_its']).sum()}")
+    # measured (MI355X, r02): mode 0 crit 8.0e-9, flow 5.6e-10 px, CG counts identical; modes 1, 2
+    # crit 2.6e-6, flow 1.3e-7 px with 3 of 46 CG counts off by one -- the reference's own
+    # last-bit sensitivity (test_reference_rounding_sensitivity: 2.6e-6), so 1e-5 there
+    crit_bar, flow_bar = (1e-7, 1e-8) if mode == 0 else (1e-5, 1e-6)
+    np.testing.assert_allclose(st["crit"], d["crit"], rtol=crit_bar, atol=0)
     for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
-        np.testing.assert_allclose(a, b, rtol=0, atol=1e-5)
+        np.testing.assert_allclose(a, b, rtol=0, atol=flow_bar)
 
 
 @pytest.mark.parametrize("env", [{"FOTO_CG_DEFER": "0"}, {"FOTO_CG_MARGIN": "-6"}, {}])
