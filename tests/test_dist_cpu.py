@@ -446,7 +446,7 @@ def _spectral_worker(rank, W, port, q, case):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W", [2, 3])
+@pytest.mark.parametrize("W", [2, 3, 5])
 def test_sharded_spectral_cg_matches_oracle(W):
     """Uneven splits on both axes (Nt = 7, Ny = 10 over 2 and 3 ranks): every rank plans the
     same steps, and the gathered phi is scipy's CG solution (iterations +-1, 5e-8 of max|x|:
