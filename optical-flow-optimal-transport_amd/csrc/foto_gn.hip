@@ -382,8 +382,14 @@ hipError_t launch_gn_pcg_upd(int w, int h, int k, const double* fx, const double
 // atomics, no ticket), and every kernel that needs the sum adds the partials in the same
 // fixed order in each of its blocks, so all blocks take identical decisions.
 
-constexpr int MG_COARSE = 1024;   // cells of the coarsest level (one block, one cell per thread)
-constexpr int MG_CSWEEPS = 48;
+#ifndef FOTO_MG_COARSE
+#define FOTO_MG_COARSE 1024
+#endif
+#ifndef FOTO_MG_CSWEEPS
+#define FOTO_MG_CSWEEPS 12   // 48 -> 12: same PCG counts at 640x480, 584x388, 320x240 (r02 A/B), 12 % less PCG time
+#endif
+constexpr int MG_COARSE = FOTO_MG_COARSE;   // cells of the coarsest level (one block, one cell per thread)
+constexpr int MG_CSWEEPS = FOTO_MG_CSWEEPS;
 constexpr double MG_OMEGA = 0.8;
 constexpr int GT_X = 32, GT_Y = 16;   // fine tile of the level kernels (256 threads, 2 cells each)
 
