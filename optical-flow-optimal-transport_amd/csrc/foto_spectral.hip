@@ -601,6 +601,9 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 #ifndef FOTO_FFT_LPB_MAX
 #define FOTO_FFT_LPB_MAX 64
 #endif
+#ifndef FOTO_FFT_SYM
+#define FOTO_FFT_SYM 1         // odd prime-length codelets by symmetric pairs (0: direct codelets)
+#endif
 #ifndef FOTO_FFT_LPB_POW2
 #define FOTO_FFT_LPB_POW2 1    // power-of-two line counts only (whole 128-B segments on strided axes)
 #endif
@@ -650,10 +653,61 @@ constexpr int dft_radix() {
     return (R % 4 == 0 && R > 4) ? 4 : (R % 2 == 0 && R > 2) ? 2 : (R % 3 == 0 && R > 3) ? 3 : (R % 5 == 0 && R > 5) ? 5 : R;
 }
 
+// Odd prime R (3, 5, 7, 19: the 640-, 480-, 420- and 380-point plans) by the symmetric pairs
+// t_j = x_j + x_{R-j}, d_j = x_j - x_{R-j} (j = 1 .. H = (R - 1) / 2):
+//   A_k = x_0 + sum_j cos(2 pi jk / R) t_j,  B_k = sum_j sin(2 pi jk / R) d_j,
+//   forward X_k = A_k - i B_k, X_{R-k} = A_k + i B_k (inverse: swapped),
+// about R real FMA per output instead of the direct codelet's 4R (roots compile-time).
+template <int R, bool INV>
+__device__ __forceinline__ void dft_sym(double (&xr)[R], double (&xi)[R]) {
+    constexpr int H = (R - 1) / 2;
+    double tr[H + 1], ti[H + 1], dr[H + 1], di[H + 1];
+    double s0r = 0.0, s0i = 0.0;
+#pragma unroll
+    for (int j = 1; j <= H; ++j) {
+        tr[j] = xr[j] + xr[R - j];
+        ti[j] = xi[j] + xi[R - j];
+        dr[j] = xr[j] - xr[R - j];
+        di[j] = xi[j] - xi[R - j];
+        s0r += tr[j];
+        s0i += ti[j];
+    }
+    double ar[H + 1], ai[H + 1], br[H + 1], bi[H + 1];
+#pragma unroll
+    for (int k = 1; k <= H; ++k) {
+        ar[k] = xr[0];
+        ai[k] = xi[0];
+        br[k] = 0.0;
+        bi[k] = 0.0;
+#pragma unroll
+        for (int j = 1; j <= H; ++j) {
+            const int p = (j * k) % R;
+            const double c = Roots<R>::re[p], sn = -Roots<R>::im[p];   // cos, sin of 2 pi p / R
+            ar[k] = fma(c, tr[j], ar[k]);
+            ai[k] = fma(c, ti[j], ai[k]);
+            br[k] = fma(sn, dr[j], br[k]);
+            bi[k] = fma(sn, di[j], bi[k]);
+        }
+    }
+    xr[0] += s0r;
+    xi[0] += s0i;
+#pragma unroll
+    for (int k = 1; k <= H; ++k) {
+        // A - i B = (ar + bi, ai - br);  A + i B = (ar - bi, ai + br)
+        const int kf = INV ? R - k : k, kb = INV ? k : R - k;
+        xr[kf] = ar[k] + bi[k];
+        xi[kf] = ai[k] - br[k];
+        xr[kb] = ar[k] - bi[k];
+        xi[kb] = ai[k] + br[k];
+    }
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void dft_reg(double (&xr)[R], double (&xi)[R]) {
     constexpr int R1 = dft_radix<R>();
-    if constexpr (R1 == R) {   // codelet: direct with compile-time roots
+    if constexpr (R1 == R && R % 2 == 1 && R > 1 && FOTO_FFT_SYM) {
+        dft_sym<R, INV>(xr, xi);
+    } else if constexpr (R1 == R) {   // codelet: direct with compile-time roots
         double yr[R], yi[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
