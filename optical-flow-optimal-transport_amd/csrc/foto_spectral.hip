@@ -2248,8 +2248,14 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
     double acc[NMOM];
 #pragma unroll
     for (int m = 0; m < NMOM; ++m) acc[m] = 0.0;
+    __shared__ double mts[NTT];   // mu_t in LDS (a global read per element after each b^ store)
+    if (threadIdx.x < NTT) mts[threadIdx.x] = T.mt[threadIdx.x];
+    __syncthreads();
     if (c < ncols) {
         const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
+        // mu_y, mu_x of the column read once: inside emit they were re-read after every b^
+        // store (the compiler cannot rule out aliasing), a dependent round trip per element
+        const double myv = T.my[ky], mxv = T.mx[kx];
         double s[H], d[H];
 #pragma unroll
         for (int j = 0; j < H; ++j) {
@@ -2259,7 +2265,7 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
         }
         auto emit = [&](int k, double X) {
             bh[k * ncols + c] = X;
-            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+            const double lam = T.reps + T.r * ((mts[k] + myv) + mxv);   // spec_lam's order
             const double x = (lam - c0) * ic1, x2 = x + x, rr = X * X;
             acc[0] += rr;
             acc[1] = fma(x, rr, acc[1]);
