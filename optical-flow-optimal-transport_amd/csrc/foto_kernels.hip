@@ -683,13 +683,16 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 // 0-2) also take the 148 ring voxels.  Chunks of FOTO_PR_TCH planes (default 16) give the
 // grid more blocks than resident slots (a full-length march leaves a one-sixth-full second
 // round at 640 x 480).
-constexpr int PR_X = 64, PR_Y = 8, PR_NT = PR_X * PR_Y;   // 512 threads
+#ifndef FOTO_PR_Y
+#define FOTO_PR_Y 8
+#endif
+constexpr int PR_X = 64, PR_Y = FOTO_PR_Y, PR_NT = PR_X * PR_Y;   // 512 threads (PR_Y 8)
 constexpr int PR_PW = PR_X + 2, PR_PH = PR_Y + 2;         // stepB region
 constexpr int PR_FW = PR_X + 4, PR_FH = PR_Y + 4;         // phi region
 constexpr int PR_HALO = 2 * PR_PW + 2 * PR_Y;             // 148 ring voxels
 constexpr int PR_FN = PR_FW * PR_FH;                      // 816 phi values per plane
 constexpr int PR_FR = (PR_FN + PR_NT - 1) / PR_NT;        // phi loads per thread per plane
-static_assert(PR_X == 64 && PR_Y == 8, "prox_rhs_blocks (foto_internal.h) assumes 64 x 8 tiles");
+static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT, "one voxel per thread, ring voxels on the first threads");
 
 __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_prox_rhs(
         Geo g, const double* __restrict__ phi, const double* __restrict__ mut, const double* __restrict__ mux,
