@@ -2235,9 +2235,16 @@ struct TCol {
 };
 
 constexpr int TC_NTH = 256;
+// Waves per SIMD of the t-column kernels (FOTO_TC_WPE, A/B builds).  At 4 (the VGPR count of the
+// Nt = 32 kernels) 1024 of the bench grid's 1200 blocks are resident; forcing 5 so the grid fits
+// in one round was measured much slower (INIT 70 -> 169 us, x^ 41 -> 98 us: the column loads
+// and the 32-point butterflies no longer fit the registers).
+#ifndef FOTO_TC_WPE
+#define FOTO_TC_WPE 4
+#endif
 
 template <int NTT>
-__global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const double* __restrict__ Ch,
+__global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_WPE))) void k_dct_t_fwd_init(SpecTab T, const double* __restrict__ Ch,
                                                            const double* __restrict__ in, double* __restrict__ bh,
                                                            SStep* Sg, RedBuf rb, double rtol, int maxiter) {
     constexpr int H = TCol<NTT>::H;
@@ -2301,7 +2308,7 @@ __global__ __launch_bounds__(TC_NTH) void k_dct_t_fwd_init(SpecTab T, const doub
 
 // Sg->k = iterations applied; 0: no pass ran, r^ was never written and r = b^ (x^ = 0)
 template <int NTT>
-__global__ __launch_bounds__(TC_NTH) void k_dct_t_inv_xhat(SpecTab T, const double* __restrict__ Ch,
+__global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_WPE))) void k_dct_t_inv_xhat(SpecTab T, const double* __restrict__ Ch,
                                                            const double* __restrict__ bh, const double* __restrict__ rh,
                                                            const SStep* Sg, double* __restrict__ out) {
     constexpr int H = TCol<NTT>::H;
