@@ -436,6 +436,32 @@ def test_full_size_cg_true_residual():
     assert np.linalg.norm(res) <= 1.01e-6 * np.linalg.norm(F)
 
 
+def test_full_size_cg_true_residual_every_outer():
+    """Bench grid, outer iterations 1..10 of the default path (deferred late-planned ring
+    passes, the interval adapted from the previous b^, the 3e4 cancellation limit): before
+    every iterate(1) read (mu, q), rebuild F with the RHS kernel (benamou_brenier.py:64-82)
+    and check the true residual of the returned phi, ||F - A phi|| <= 1.01 * rtol * ||F||
+    (scipy's stop rule, benamou_brenier.py:85).  The chunked run's crit sequence must equal
+    one iterate(10) call's, so the fused prox+RHS head of the chunked path is covered too."""
+    from foto.synthetic import translating_gaussian
+    Nt, Ny, Nx, K = 32, 480, 640, 10
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    ratios = []
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
+        for _ in range(K):
+            mu, q = s.state()
+            s.iterate(1, 0.0, False)
+            F = ops.bb_rhs(mu, q, rho0, rhoT, 1.0, Nt, Nx, Ny)
+            res = F - ops.apply_A(s.phi(), Nt, Nx, Ny, 1.0, 1e-2)
+            ratios.append(np.linalg.norm(res) / (1e-6 * np.linalg.norm(F)))
+        crit_chunked = np.array(s.crit)
+    print("true residual / (rtol ||F||) per outer:", np.round(ratios, 4))
+    assert max(ratios) <= 1.01, ratios
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
+        s.iterate(K, 0.0, False)
+        np.testing.assert_allclose(np.array(s.crit), crit_chunked, rtol=1e-9)
+
+
 # ---------------------------------------------------------------- DCT axis transforms
 
 @pytest.mark.parametrize("n", [8, 32, 64, 128, 146, 194, 256, 380, 388, 420, 480, 512, 584, 640, 1024])
