@@ -2088,12 +2088,18 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
     constexpr bool LATE = FUSE && !INIT;
     __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
     __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
+    // A late-planning pass needs the previous pass's moments: their loads are issued before the
+    // state's, so the two round trips overlap instead of running back to back (the plan waits
+    // for both).  The asm use pins the loads above the state checks.
+    __shared__ double tot[NACC];
+    double gpre = 0.0;
+    if (LATE && threadIdx.x < NACC) gpre = gath[threadIdx.x];   // rank 0's slot
     SStep S0 = *Sg;
+    if (LATE && threadIdx.x < NACC) tot[threadIdx.x] = gpre;    // (waits for the moments only)
     if (!INIT && S0.done) return;
     const bool late = LATE && S0.pend;
     if (!INIT && !late && S0.nsteps == 0) return;
     double* tab = ring + RING_NW * D * RING_SLOT;
-    __shared__ double tot[NACC];
     const RingWave w = ring_wave(T, ring, D);
     int issued = 0;
     if constexpr (LATE) {
@@ -2109,9 +2115,11 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
             const long long c0 = wall_clock64();
 #endif
             if (threadIdx.x < 64) {
-                if (threadIdx.x < NACC) {   // the ranks' moments, summed in rank order (k_spec_s2_plan's)
-                    double t = 0.0;
-                    for (int g = 0; g < world; ++g) t += gath[g * NACC + threadIdx.x];
+                // the ranks' moments, summed in rank order (k_spec_s2_plan's: 0 + g0 = g0), rank
+                // 0's loaded at entry
+                if (threadIdx.x < NACC && world > 1) {
+                    double t = gpre;
+                    for (int g = 1; g < world; ++g) t += gath[g * NACC + threadIdx.x];
                     tot[threadIdx.x] = t;
                 }
                 if (threadIdx.x == 0) Sl = S0;

@@ -21,8 +21,58 @@ __global__ __launch_bounds__(256) void stream_rq(double* __restrict__ r, double*
     }
 }
 
-int main() {
-    const int Nt = 32, Ny = 480, Nx = 640;
+
+// Kernel-boundary cost: npass ring passes in ONE launch (each block keeps its tiles and its
+// LDS tables across passes), optionally with a grid-wide arrival counter between passes (the
+// synchronisation a persistent solve needs for its moments).  The spin is bounded by the
+// 100 MHz wall clock, so a non-resident grid cannot hang the box.
+__device__ int lab_err;
+template <int D>
+__global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))) void k_lab_multi(
+        SpecTab T, double* __restrict__ rh, double* __restrict__ ph, const double* __restrict__ bh, const SStep* Sg,
+        double* out, unsigned* ctr, int npass, int gsync) {
+    __shared__ __attribute__((aligned(16))) double ring[RING_NW * D * RING_SLOT + RING_TAB];
+    __shared__ double wred[RING_NW * NACC];
+    __shared__ double tot[NACC];
+    const SStep S0 = *Sg;
+    double* tab = ring + RING_NW * D * RING_SLOT;
+    const RingWave w = ring_wave(T, ring, D);
+    ring_stage_tables(T, tab);
+    __syncthreads();
+    for (int p = 0; p < npass; ++p) {
+        double acc[NACC];
+#pragma unroll
+        for (int m = 0; m < NACC; ++m) acc[m] = 0.0;
+        ring_pass<D, false>(T, w, lds_u32(tab), S0, rh, ph, bh, acc, 0, true);
+        blk_sum_rs<NACC, S2_NTH>(acc, wred, tot);
+        if (threadIdx.x < NACC)
+            __hip_atomic_store(&out[(int64_t)threadIdx.x * gridDim.x + blockIdx.x], tot[threadIdx.x], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef LAB_NOFENCE
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+        if (gsync) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned target = (unsigned)(p + 1) * gridDim.x;
+                const long long t0 = wall_clock64();
+                while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (wall_clock64() - t0 > 100000000LL) { lab_err = 1; break; }   // 1 s
+                }
+            }
+            __syncthreads();
+        }
+#ifndef LAB_NOFENCE
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    }
+}
+
+int main(int argc, char** argv) {
+    const int Nt = argc > 1 ? atoi(argv[1]) : 32, Ny = 480, Nx = 640;   // Nt sweep: fixed cost per pass
     const size_t n = (size_t)Nt * Ny * Nx;
     std::vector<double> mt(Nt), my(Ny), mx(Nx);
     for (int k = 0; k < Nt; ++k) mt[k] = 2 - 2 * cos(M_PI * k / Nt);
@@ -61,7 +111,7 @@ int main() {
         (void)hipMemcpy(Sg, &S0, sizeof(SStep), hipMemcpyHostToDevice);
         (void)hipMemcpy(Sg2, &S0, sizeof(SStep), hipMemcpyHostToDevice);
     };
-    printf("SMAX=%d S2_NTH=%d ring D=%d\n", SMAX, S2_NTH, FOTO_RING_D);
+    printf("SMAX=%d S2_NTH=%d ring D=%d grid %dx%dx%d\n", SMAX, S2_NTH, FOTO_RING_D, Nx, Ny, Nt);
     // correctness: one pass each from the same state, moments to gath (no fused plan)
     reset();
     const int G = 256;
@@ -115,6 +165,40 @@ int main() {
     }
     timeit("ring INIT, moments only", [&] { (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, true, false, 0); });
     timeit("product INIT, moments only", [&] { k_spec_s2<true, true, false><<<256, S2_NTH>>>(T, r, p, b, Sg, rb, 1e-6, 1000, gath, 0); });
+
+    {   // one launch, 20 passes: no grid sync / with the arrival counter
+        for (int np : {1, 2, 4}) {
+            float best = 1e9;
+            for (int rep = 0; rep < 5; ++rep) {
+                (void)hipEventRecord(e0);
+                k_lab_multi<FOTO_RING_D><<<256, S2_NTH>>>(T, r2, p2, b, Sg2, part, ticket, np, 0);
+                (void)hipEventRecord(e1);
+                (void)hipEventSynchronize(e1);
+                float t;
+                (void)hipEventElapsedTime(&t, e0, e1);
+                if (t < best) best = t;
+            }
+            printf("persistent ring, %d passes, no grid sync     %6.1f us per pass\n", np, best * 1e3 / np);
+        }
+        for (int gs = 0; gs < 2; ++gs) {
+            float best = 1e9;
+            for (int rep = 0; rep < 5; ++rep) {
+                (void)hipMemset(ticket, 0, 256);
+                (void)hipEventRecord(e0);
+                k_lab_multi<FOTO_RING_D><<<256, S2_NTH>>>(T, r2, p2, b, Sg2, part, ticket, 20, gs);
+                (void)hipEventRecord(e1);
+                (void)hipEventSynchronize(e1);
+                float t;
+                (void)hipEventElapsedTime(&t, e0, e1);
+                if (t < best) best = t;
+            }
+            int herr = 0;
+            (void)hipMemcpyFromSymbol(&herr, HIP_SYMBOL(lab_err), sizeof herr);
+            printf("%-44s %6.1f us per pass (one launch of 20%s)\n", gs ? "persistent ring, grid counter" : "persistent ring, no grid sync",
+                   best * 1e3 / 20, herr ? ", SPIN TIMEOUT" : "");
+        }
+        (void)hipMemset(ticket, 0, 256);
+    }
     auto single = [&](const char* name, auto launch) {
         float best = 1e9;
         for (int rep = 0; rep < 20; ++rep) {

@@ -19,3 +19,11 @@ for d in sys.argv[1:]:
     gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(rows, rows[1:])]
     g = np.array(gaps)
     print(f"  gaps: total {g.sum():.0f} us, median {np.median(g):.2f}, >20us: {int((g > 20).sum())} totalling {g[g > 20].sum():.0f} us")
+    # gaps by (previous kernel -> next kernel), the most frequent pairs
+    pairs = collections.defaultdict(list)
+    short = lambda r: r["Kernel_Name"].split("(")[0].split("<")[0].replace("foto::", "").replace("void ", "")
+    for a, b, gp in zip(rows, rows[1:], gaps):
+        pairs[(short(a), short(b))].append(gp)
+    for (a, b), v in sorted(pairs.items(), key=lambda kv: -len(kv[1]))[:8]:
+        v = np.array(v)
+        print(f"  gap {a} -> {b}: n={len(v)} median {np.median(v):.2f} us, p10 {np.percentile(v,10):.2f}, p90 {np.percentile(v,90):.2f}")
