@@ -1924,18 +1924,36 @@ __device__ __forceinline__ void ring_stage_tables(const SpecTab& T, double* tab,
         tab[i] = (i < T.Nx) ? T.mx[i] : (i < T.Nx + T.Nt) ? T.mt[i - T.Nx] : T.my[T.y0 + i - T.Nx - T.Nt];
 }
 
-// The wave's tile sequence: u = gw + j W (j < nj), u -> (row, 128-column segment cx).
+// The wave's tile sequence: u = gw + j W (j < nj), u -> (row, 128-column segment cx) when the
+// rows are whole tiles (Nx % 128 == 0); otherwise the box is tiled flat (tile u = elements
+// [128 u, 128 u + 128) of the contiguous [t][y][x] box, rows found per lane), so row lengths
+// like Middlebury's 584 (4.56 tiles) or 420 (3.28) leave no idle lanes in a last segment.
 struct RingWave {
     int gw, W, nj, ntx;
+    bool flat;
+    int nel;         // elements of the box (flat tiling)
     double* wring;   // this wave's D slots
 };
+
+// floor(e / n) and the remainder, 0 <= e < 2^31, quotient < 2^17: the fp32 estimate is within
+// one of the quotient, and one correction each way makes it exact
+__device__ __forceinline__ int ring_divmod(int e, int n, float inv, int* rem) {
+    int q = (int)((float)e * inv);
+    int r = e - q * n;
+    if (r < 0) { --q; r += n; }
+    else if (r >= n) { ++q; r -= n; }
+    *rem = r;
+    return q;
+}
 
 __device__ __forceinline__ RingWave ring_wave(const SpecTab& T, double* ring, int D) {
     RingWave w;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int rows = T.Nt * T.nyl;
     w.ntx = (T.Nx + 127) / 128;
-    const int nwt = rows * w.ntx;
+    w.flat = (T.Nx % 128) != 0;
+    w.nel = rows * T.Nx;
+    const int nwt = w.flat ? (w.nel + 127) / 128 : rows * w.ntx;
     w.gw = blockIdx.x * RING_NW + wv;
     w.W = gridDim.x * RING_NW;
     w.nj = w.gw < nwt ? (nwt - 1 - w.gw) / w.W + 1 : 0;
@@ -1949,10 +1967,16 @@ __device__ __forceinline__ void ring_issue(const SpecTab& T, const RingWave& w, 
                                            const double* ph, bool loadq) {
     const int lane = threadIdx.x & 63;
     const int u = w.gw + j * w.W;
-    const int row = u / w.ntx, cx = u - row * w.ntx;
-    int kx = cx * 128 + 2 * lane;
-    if (kx >= T.Nx) kx = cx * 128;   // idle lanes fetch a valid address; never read
-    const int64_t i = (int64_t)row * T.Nx + kx;
+    int64_t i;
+    if (w.flat) {
+        const int e = u * 128 + 2 * lane;
+        i = (e < w.nel) ? e : u * 128;   // idle lanes fetch a valid address; never read
+    } else {
+        const int row = u / w.ntx, cx = u - row * w.ntx;
+        int kx = cx * 128 + 2 * lane;
+        if (kx >= T.Nx) kx = cx * 128;
+        i = (int64_t)row * T.Nx + kx;
+    }
     double* slot = w.wring + (j % D) * RING_SLOT;
     __builtin_amdgcn_global_load_lds((const void*)(src + i), (lds_void_t*)slot, 16, 0, 0);
     if (loadq) __builtin_amdgcn_global_load_lds((const void*)(ph + i), (lds_void_t*)(slot + 128), 16, 0, 0);
@@ -1992,6 +2016,7 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
         }
     };
     const int nj = w.nj;
+    const float invx = 1.0f / (float)T.Nx, invy = 1.0f / (float)T.nyl;
     const int g = loadq ? 2 : 1;             // DMA instructions per tile
     constexpr int NS = INIT ? 1 : 2;         // store instructions per tile
     for (int j = issued; j < D - 1 && j < nj; ++j) ring_issue<D>(T, w, j, src, ph, loadq);
@@ -2007,15 +2032,29 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
             vm_wait(g * nG + NS * nS);
         }
         const int u = w.gw + j * w.W;
-        const int row = u / w.ntx, cx = u - row * w.ntx;
-        const int kx = cx * 128 + 2 * lane;
+        int kx, kt, ky;
+        bool ok;
+        int64_t i;
+        if (w.flat) {   // per lane: element e -> (row, kx) -> (kt, ky)
+            const int e0 = u * 128 + 2 * lane;
+            ok = e0 < w.nel;
+            const int e = ok ? e0 : u * 128;
+            const int row = ring_divmod(e, T.Nx, invx, &kx);
+            kt = ring_divmod(row, T.nyl, invy, &ky);
+            i = e;
+        } else {
+            const int row = u / w.ntx, cx = u - row * w.ntx;
+            kx = cx * 128 + 2 * lane;
+            kt = row / T.nyl;
+            ky = row - kt * T.nyl;
+            ok = kx < T.Nx;
+            i = (int64_t)row * T.Nx + kx;
+        }
         const unsigned sa = lds_u32(w.wring + (j % D) * RING_SLOT) + 16 * lane;
         dbl2 rv = lds_ld128(sa);
         dbl2 qv = loadq ? lds_ld128(sa + 1024) : dbl2{0.0, 0.0};
-        const int kt = row / T.nyl, ky = row - kt * T.nyl;
         double mtv = lds_ld64(tab_a + 8 * (T.Nx + kt));
         double myv = lds_ld64(tab_a + 8 * (T.Nx + T.Nt + ky));
-        const bool ok = kx < T.Nx;
         dbl2 mxv = lds_ld128(tab_a + 8 * (ok ? kx : 0));
         // the wait names every asm-loaded register, so no use is scheduled above it
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rv), "+v"(qv), "+v"(mtv), "+v"(myv), "+v"(mxv) :: "memory");
@@ -2023,7 +2062,6 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
         const double l0 = T.reps + T.r * (rowmu + mxv[0]);
         const double l1 = T.reps + T.r * (rowmu + mxv[1]);
         double r0 = rv[0], r1 = rv[1], q0 = qv[0], q1 = qv[1];
-        const int64_t i = (int64_t)row * T.Nx + kx;
         if (INIT) {
             if (ok) *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
         } else {
