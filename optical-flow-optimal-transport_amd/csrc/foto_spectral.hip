@@ -1912,9 +1912,11 @@ __device__ __forceinline__ void vm_wait(int k) {
     }
 }
 
-// Usable for a shard when Nx is even (16-B lanes) and the tables fit.
+// Usable for a shard when Nx is even (16-B lanes), the tables fit and the box's element
+// indices stay in 30 bits (32-bit tile and element arithmetic; ring_divmod's quotients, at
+// most Nt * nyl < 2^21 under the table bound, are exact).
 static inline bool ring_ok(const SpecTab& T) {
-    return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB;
+    return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB && (int64_t)T.Nt * T.nyl * T.Nx < (int64_t(1) << 30);
 }
 
 // Tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl).
@@ -1935,8 +1937,8 @@ struct RingWave {
     double* wring;   // this wave's D slots
 };
 
-// floor(e / n) and the remainder, 0 <= e < 2^31, quotient < 2^17: the fp32 estimate is within
-// one of the quotient, and one correction each way makes it exact
+// floor(e / n) and the remainder, 0 <= e < 2^30, quotient < 2^21: the fp32 estimate is off by
+// less than (e / n) 2^-21.7 + 1 < 2, and one correction each way makes it exact
 __device__ __forceinline__ int ring_divmod(int e, int n, float inv, int* rem) {
     int q = (int)((float)e * inv);
     int r = e - q * n;
