@@ -8,6 +8,11 @@
   Dimetrodon's 584x388) and the full 584x388x32 grid (mode 2 vs the literal stencil CG, true
   residual).
 * C3: GN at 640x480 against the reference's SuperLU solve (gn_c3.npz) and its own residual.
+* C4 size 1024x1024x64 on one device: the default spectral CG against the literal stencil CG
+  and its true residual, and the 8-shard decomposition of the 8-GPU config through the
+  transfer lists RCCL executes (no reference golden: the reference needs hours per outer
+  iteration at this size; the stencil CG is the reference's algorithm, tested against the
+  goldens at the smaller sizes).
 
 Bars (float64), set ~30x above what the MI355X measured (printed with -s):
   * CG counts +-1 (a residual norm can land within rounding of atol);
@@ -16,7 +21,9 @@ Bars (float64), set ~30x above what the MI355X measured (printed with -s; DESIGN
   * C2-shaped golden: crit 1e-8, phi 1e-8, flow 1e-8 px (measured <= 2.6e-10 / 1.4e-10);
   * C2 full size, spectral vs stencil: crit 1e-8, phi 1e-8 (measured 3.3e-10 / 1.3e-10);
   * true residuals <= 1.01 rtol ||F|| (scipy's rule is on the recursive residual);
-  * GN 640x480 vs SuperLU: 1e-8 (measured 8.2e-10), relative residual <= 1.01e-10.
+  * GN 640x480 vs SuperLU: 1e-8 (measured 8.2e-10), relative residual <= 1.01e-10;
+  * C4 size: spectral vs stencil crit 1e-7, phi 1e-8 (measured 2.7e-9 / 3.5e-10); 8 shards vs
+    one crit 1e-7, phi 1e-6 (the bench-grid shard bars; measured 2.8e-15 / 1.1e-15).
 """
 import numpy as np
 import pytest
@@ -152,3 +159,35 @@ def test_gn_c3_vs_reference(gold):
     print(f"GN 640x480: {its} PCG its, relative residual {res:.2e}, max |d| u v m {errs}")
     assert res <= 1.01e-10
     assert max(errs) <= 1e-8
+
+
+def test_c4_full_size():
+    """C4 size 1024x1024x64 (BASELINE configs[3]) on one device, two outer iterations: the
+    default spectral s-step CG (Nt = 64: the t axis by the strided FFT) against the literal
+    stencil CG, the true residual of each default solve, and 8 in-process shards -- the
+    8-GPU decomposition, 8 planes and 128 rows per rank -- against the single shard."""
+    Nt, Nx, Ny, r, eps = 64, 1024, 1024, 1.0, 1e-2
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = {}
+    for key, mode, vr in (("spectral", 2, 1), ("stencil", 0, 1), ("spectral x8", 2, 8)):
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode, virtual_ranks=vr) as s:
+            rels = []
+            if vr == 1 and mode == 2:
+                for _ in range(2):
+                    mu, q = s.state()
+                    s.iterate(1, 0.0, False)
+                    rels.append(_true_residual_ok(s, mu, q, rho0, rhoT, Nt, Nx, Ny, r, eps))
+                    del mu, q
+            else:
+                s.iterate(2, 0.0, False)
+            out[key] = (np.array(s.cg_its), np.array(s.crit), s.phi(), rels)
+    (k2, c2, p2, r2), (k0, c0, p0, _), (k8, c8, p8, _) = (out[k] for k in ("spectral", "stencil", "spectral x8"))
+    print(f"C4 cg stencil {k0.tolist()} spectral {k2.tolist()} x8 {k8.tolist()}; spectral vs stencil crit rel "
+          f"{_rel(c2, c0):.2e} phi rel {_rel(p2, p0):.2e}; x8 vs one crit rel {_rel(c8, c2):.2e} phi rel "
+          f"{_rel(p8, p2):.2e}; true residuals {r2}")
+    assert max(r2) <= 1.01 * RTOL_CG
+    assert np.max(np.abs(k0 - k2)) <= 1 and np.max(np.abs(k8 - k2)) <= 1
+    np.testing.assert_allclose(c2, c0, rtol=1e-7)
+    assert _rel(p2, p0) <= 1e-8
+    np.testing.assert_allclose(c8, c2, rtol=1e-7)
+    assert _rel(p8, p2) <= 1e-6
