@@ -1,10 +1,10 @@
 # Experiment (CPU, test infrastructure: imports the oracle and the numpy plan restatement).
-# usage: python tools/cs_bound_exp.py exact|cs 80x60x32 [limit]
+# usage: python tests/cs_bound_exp.py exact|cs 80x60x32 [limit]
 # Pass counts of the s-step plan with the exact |terms| cancellation ratio vs the Cauchy-Schwarz
 # bound (|H_ac| <= sqrt(H_aa H_cc)), on the first BB solve of a translating-Gaussian pair.
 import sys, math, time
 import numpy as np
-sys.path.insert(0, "/root/repo/tests"); sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/optical-flow-optimal-transport_amd")
+import os; _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path[:0] = [os.path.join(_R, "tests"), _R, os.path.join(_R, "optical-flow-optimal-transport_amd")]
 import test_sstep_plan as T
 from oracle import foto_oracle as O
 from foto.synthetic import translating_gaussian
