@@ -146,12 +146,35 @@ int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny
 /* RCCL unique id for foto_bb_opts.nccl_id (call on rank 0, broadcast 128 bytes). */
 int foto_nccl_unique_id(void* out128);
 
+/* Test entry (host only, no device): the point-to-point calls rank `rank` of `world` issues
+ * over RCCL for one exchange of the time-sharded solve (the loop of benamou_brenier.py:204-258
+ * split into time slabs), in issue order.  Each call is 5 int64:
+ * {op (FOTO_CALL_*), peer, offset, count, copy destination offset}, offsets in doubles from
+ * the buffer the exchange picks (send / copy: source; recv: destination).  Sends and receives
+ * go in one ncclGroupStart/End; copies follow the group.  arg: the relay step j (RELAY).    */
+#define FOTO_XFER_HALO 0          /* halo planes of a slab field (plane -1 / nloc)            */
+#define FOTO_XFER_SLAB_TO_BOX 1   /* spectral all-to-all: time slabs -> row boxes             */
+#define FOTO_XFER_BOX_TO_SLAB 2   /* spectral all-to-all: row boxes -> time slabs             */
+#define FOTO_XFER_RELAY 3         /* trajectory positions rank j -> j + 1 (flow extraction)   */
+#define FOTO_XFER_DELIVER 4       /* (u, v, m) last rank -> rank 0                            */
+#define FOTO_CALL_SEND 0
+#define FOTO_CALL_RECV 1
+#define FOTO_CALL_COPY 2
+int foto_xfer_calls(int kind, int Nt, int Ny, int Nx, int world, int rank, int arg, int64_t* out, int cap,
+                    int* count);
+
 /* Test entry: the orthonormal DCT-II (inverse = 0) or DCT-III (inverse = 1) along the middle
  * axis of a C-order [outer][n][inner] array, as scipy.fft.dct(x, type=2|3, norm="ortho",
  * axis=1) -- the transform pair that diagonalises lap1d (operators.py:33-48) in the spectral
  * CG.  path 0: the FFT kernels when n has a plan, else the MFMA GEMM kernels; 1: FFT only
  * (error without a plan); 2: GEMM only.                                            */
 int foto_dct(const double* in, int outer, int n, int inner, int inverse, int path, double* out);
+
+/* Measurement entry (bench.py): the dominant s-step pass's memory traffic alone -- read and
+ * write two n-double vectors, 16 B per lane, no arithmetic beyond one update -- timed over
+ * `reps` back-to-back launches on this device; us[0] plain stores, us[1] write-through (sc1)
+ * stores, microseconds per launch (best of 3).  n even, n * 8 < 2^31.                   */
+int foto_stream_probe(int64_t n, int reps, double* us);
 
 /* ------------------------------------------------------------------ GN baseline
  * classical.GLLOpticalFlow (classical.py:25-130).                                 */

@@ -77,16 +77,11 @@ class GLLOpticalFlow(object):
 
     def process(self):
         """Solve for [u, v, m] on the GPU.  The solver plan (device buffers, multigrid levels,
-        the replayed PCG graph) is kept on the instance and reused while (w, h, alpha, lambda,
-        rtol, maxiter) stay the same."""
-        key = (self.w, self.h, self.alpha, self.lambdap, self.rtol, self.maxiter)
-        if getattr(self, "_plan_key", None) != key:
-            old = getattr(self, "_plan", None)
-            if old is not None:
-                old.close()
-            self._plan = _gn.Plan(self.w, self.h, self.alpha, self.lambdap, self.rtol, self.maxiter)
-            self._plan_key = key
-        u, v, m, info, its = self._plan.solve(self.f1, self.f2)
+        the replayed PCG graph) comes from a process-wide cache keyed by (w, h, alpha, lambda,
+        rtol, maxiter) (foto.gn.cached_plan), so every instance with the same size and
+        parameters -- a batch of frames -- shares one."""
+        plan = _gn.cached_plan(self.w, self.h, self.alpha, self.lambdap, self.rtol, self.maxiter)
+        u, v, m, info, its = plan.solve(self.f1, self.f2)
         self.iterations = its
         if info > 0:
             # stderr: the reference (spsolve) never prints here, so stdout stays identical

@@ -17,6 +17,7 @@
 
 #include "foto_internal.h"
 #include "foto_spectral.h"
+#include "foto_xfer.h"
 
 namespace foto {
 
@@ -87,13 +88,6 @@ struct Shard {
     }
 };
 
-static int split_planes(int Nt, int W, int rank, int* t0, int* nloc) {
-    const int base = Nt / W, extra = Nt % W;
-    *nloc = base + (rank < extra ? 1 : 0);
-    *t0 = rank * base + std::min(rank, extra);
-    return *nloc >= 1 ? 0 : -1;
-}
-
 }  // namespace foto
 
 using namespace foto;
@@ -144,20 +138,16 @@ struct foto_bb_ctx {
 namespace foto {
 
 // ----------------------------------------------------------------------------- communication
-// Every exchange between shards is a list of point-to-point transfers, built by the same
-// code on every rank and for every transport; only its execution differs:
+// Every exchange between shards is a list of point-to-point transfers (foto_xfer.h), built by
+// the same code on every rank and for every transport; only its execution differs:
 //   virtual ranks (one process, all shards on one device and stream): one device copy per
 //   transfer, in list order;
-//   RCCL (one shard per process): in one group, ncclSend for each transfer from this rank and
-//   ncclRecv for each transfer to it (pairs match in list order, which is the same on every
-//   rank); a transfer to itself is a device copy.
+//   RCCL (one shard per process): the calls rccl_calls() lists -- in one group, ncclSend for
+//   each transfer from this rank and ncclRecv for each transfer to it (pairs match in list
+//   order, which is the same on every rank), then a device copy for each transfer to itself.
 // Offsets are in doubles from the pointer a picker returns for the shard (negative: the halo
-// plane below).  The virtual-rank GPU tests therefore run the very lists RCCL executes.
-struct Xfer {
-    int src, dst;
-    int64_t soff, doff, n;
-};
-
+// plane below).  The virtual-rank GPU tests therefore run the very lists RCCL executes, and
+// tests/test_xfer.py checks the RCCL call sequences of every rank against each other.
 template <class SrcPick, class DstPick>
 static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, DstPick dp) {
     if (!c->rccl) {
@@ -167,23 +157,24 @@ static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, Dst
         return 0;
     }
     Shard& s = *c->sh[0];
-    const int me = s.rank;
-    bool any = false;
-    for (const Xfer& x : xs) any = any || ((x.src == me) != (x.dst == me));
-    if (any) {
-        FOTO_NCCL_CHECK(ncclGroupStart());
-        for (const Xfer& x : xs) {
-            if (x.src == me && x.dst != me)
-                FOTO_NCCL_CHECK(ncclSend(sp(s) + x.soff, (size_t)x.n, ncclDouble, x.dst, c->nc, c->s));
-            if (x.dst == me && x.src != me)
-                FOTO_NCCL_CHECK(ncclRecv(dp(s) + x.doff, (size_t)x.n, ncclDouble, x.src, c->nc, c->s));
+    const std::vector<Call> cs = rccl_calls(xs, s.rank);
+    const bool grouped = !cs.empty() && cs.front().op != CALL_COPY;
+    if (grouped) FOTO_NCCL_CHECK(ncclGroupStart());
+    bool open = grouped;
+    for (const Call& k : cs) {
+        if (k.op == CALL_COPY && open) {
+            FOTO_NCCL_CHECK(ncclGroupEnd());
+            open = false;
         }
-        FOTO_NCCL_CHECK(ncclGroupEnd());
-    }
-    for (const Xfer& x : xs)
-        if (x.src == me && x.dst == me)
-            FOTO_HIP_CHECK(hipMemcpyAsync(dp(s) + x.doff, sp(s) + x.soff, (size_t)x.n * sizeof(double),
+        if (k.op == CALL_SEND)
+            FOTO_NCCL_CHECK(ncclSend(sp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, c->s));
+        else if (k.op == CALL_RECV)
+            FOTO_NCCL_CHECK(ncclRecv(dp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, c->s));
+        else
+            FOTO_HIP_CHECK(hipMemcpyAsync(dp(s) + k.doff, sp(s) + k.off, (size_t)k.n * sizeof(double),
                                           hipMemcpyDeviceToDevice, c->s));
+    }
+    if (open) FOTO_NCCL_CHECK(ncclGroupEnd());
     return 0;
 }
 
@@ -198,21 +189,13 @@ static int allgather(foto_bb_ctx* c, Pick pick, int cnt) {
         FOTO_NCCL_CHECK(ncclAllGather(base + (size_t)s.rank * cnt, base, cnt, ncclDouble, c->nc, c->s));
         return 0;
     }
-    std::vector<Xfer> xs;
-    for (int g = 0; g < c->W; ++g)
-        for (int h = 0; h < c->W; ++h)
-            if (g != h) xs.push_back({g, h, (int64_t)g * cnt, (int64_t)g * cnt, cnt});
-    return exchange(c, xs, pick, pick);
+    return exchange(c, allgather_xfers(c->W, cnt), pick, pick);
 }
-
-// halo planes of a halo-padded field: plane -1 <- previous rank's last plane, plane nloc <-
-// next rank's first plane
-static std::vector<Xfer> halo_xfers(const foto_bb_ctx* c);
 
 template <class Pick>
 static int halo(foto_bb_ctx* c, Pick pick) {
     if (c->W == 1) return 0;
-    return exchange(c, halo_xfers(c), pick, pick);
+    return exchange(c, halo_xfers(c->Nt, (int64_t)c->Nx * c->Ny, c->W), pick, pick);
 }
 
 // ----------------------------------------------------------------------------- context setup
@@ -281,18 +264,6 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     return 0;
 }
 
-static std::vector<Xfer> halo_xfers(const foto_bb_ctx* c) {
-    std::vector<Xfer> xs;
-    const int64_t nxy = (int64_t)c->Nx * c->Ny;
-    for (int j = 0; j + 1 < c->W; ++j) {
-        int t0, nl;
-        split_planes(c->Nt, c->W, j, &t0, &nl);
-        xs.push_back({j, j + 1, (int64_t)(nl - 1) * nxy, -nxy, nxy});   // up: last plane -> halo below
-        xs.push_back({j + 1, j, 0, (int64_t)nl * nxy, nxy});             // down: first plane -> halo above
-    }
-    return xs;
-}
-
 // ----------------------------------------------------------------------------- CG driver
 
 static CGArgs cg_args(foto_bb_ctx* c, const Shard& s) {
@@ -341,34 +312,11 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
     return 0;
 }
 
-// all-to-all between the physical slabs and the spectral row boxes (SpectralPlan):
-//   forward : rank g sends stage_g[nloc_g*Nx*y0_h, + nloc_g*nyl_h*Nx]  -> box_in_h[t0_g*nyl_h*Nx, ...]
-//   backward: rank g sends box_out_g[t0_h*nyl_g*Nx, + nloc_h*nyl_g*Nx] -> stage_h[nloc_h*Nx*y0_g, ...]
+// all-to-all between the physical slabs and the spectral row boxes (foto_xfer.h)
 static int alltoall_spec(foto_bb_ctx* c, bool forward) {
-    const int W = c->W;
-    const int64_t Nx = c->Nx;
-    auto slab = [&](int h, int* t0, int* nl) { split_planes(c->Nt, W, h, t0, nl); };
-    auto rows = [&](int h, int* y0, int* ny) { split_planes(c->Ny, W, h, y0, ny); };
-    // region rank a sends to rank b (and b receives from a), in doubles
-    auto region = [&](int a, int b, int64_t* soff, int64_t* roff, int64_t* cnt) {
-        int ta, na, tb, nb, ya, nya, yb, nyb;
-        slab(a, &ta, &na); slab(b, &tb, &nb); rows(a, &ya, &nya); rows(b, &yb, &nyb);
-        if (forward) {
-            *soff = (int64_t)na * Nx * yb; *cnt = (int64_t)na * nyb * Nx; *roff = (int64_t)ta * nyb * Nx;
-        } else {
-            *soff = (int64_t)tb * nya * Nx; *cnt = (int64_t)nb * nya * Nx; *roff = (int64_t)nb * Nx * ya;
-        }
-    };
     auto sbuf = [&](Shard& s) { return forward ? s.spec->stage() : s.spec->box_out(); };
     auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.spec->stage(); };
-    std::vector<Xfer> xs;
-    for (int a = 0; a < W; ++a)
-        for (int b = 0; b < W; ++b) {
-            int64_t so, ro, n;
-            region(a, b, &so, &ro, &n);
-            if (n > 0) xs.push_back({a, b, so, ro, n});
-        }
-    return exchange(c, xs, sbuf, rbuf);
+    return exchange(c, alltoall_xfers(c->Nt, c->Ny, c->Nx, c->W, forward), sbuf, rbuf);
 }
 
 // Spectral s-step CG over time-slab shards: x/y DCTs on the own planes, all-to-all to
@@ -614,13 +562,13 @@ static int flow(foto_bb_ctx* c, double* u, double* v, double* m) {
             if (j == W - 1) FOTO_HIP_CHECK(launch_flow_finish(c->Nx, c->Ny, s->px, s->py, s->fu, s->fv, s->fm, c->s));
         }
         if (j + 1 < W) {
-            const std::vector<Xfer> xs = {{j, j + 1, 0, 0, nxy}};
+            const std::vector<Xfer> xs = relay_xfers(nxy, j);
             FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.px; }, [](Shard& s) { return s.px; }));
             FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.py; }, [](Shard& s) { return s.py; }));
         }
     }
     if (W > 1) {
-        const std::vector<Xfer> xs = {{W - 1, 0, 0, 0, nxy}};
+        const std::vector<Xfer> xs = deliver_xfers(nxy, W);
         FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fu; }, [](Shard& s) { return s.fu; }));
         FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fv; }, [](Shard& s) { return s.fv; }));
         FOTO_TRY(exchange(c, xs, [](Shard& s) { return s.fm; }, [](Shard& s) { return s.fm; }));
@@ -666,6 +614,35 @@ int foto_bb_opts_default(foto_bb_opts* o) {
     o->nccl_id = nullptr;
     o->virtual_ranks = 1;
     o->timing = 0;
+    return 0;
+}
+
+int foto_xfer_calls(int kind, int Nt, int Ny, int Nx, int world, int rank, int arg, int64_t* out, int cap,
+                    int* count) {
+    if (!out || !count || world < 1 || rank < 0 || rank >= world || Nt < world || Ny < world || Nx < 1) {
+        set_error("foto_xfer_calls: bad arguments");
+        return FOTO_ERR_ARG;
+    }
+    const int64_t nxy = (int64_t)Nx * Ny;
+    std::vector<Xfer> xs;
+    switch (kind) {
+        case FOTO_XFER_HALO: xs = halo_xfers(Nt, nxy, world); break;
+        case FOTO_XFER_SLAB_TO_BOX: xs = alltoall_xfers(Nt, Ny, Nx, world, true); break;
+        case FOTO_XFER_BOX_TO_SLAB: xs = alltoall_xfers(Nt, Ny, Nx, world, false); break;
+        case FOTO_XFER_RELAY:
+            if (arg < 0 || arg + 1 >= world) { set_error("foto_xfer_calls: relay step out of range"); return FOTO_ERR_ARG; }
+            xs = relay_xfers(nxy, arg);
+            break;
+        case FOTO_XFER_DELIVER: xs = deliver_xfers(nxy, world); break;
+        default: set_error("foto_xfer_calls: unknown kind %d", kind); return FOTO_ERR_ARG;
+    }
+    const std::vector<Call> cs = rccl_calls(xs, rank);
+    *count = (int)cs.size();
+    if ((int)cs.size() > cap) { set_error("foto_xfer_calls: %d calls, capacity %d", (int)cs.size(), cap); return FOTO_ERR_ARG; }
+    for (size_t i = 0; i < cs.size(); ++i) {
+        int64_t* o = out + 5 * i;
+        o[0] = cs[i].op; o[1] = cs[i].peer; o[2] = cs[i].off; o[3] = cs[i].n; o[4] = cs[i].doff;
+    }
     return 0;
 }
 

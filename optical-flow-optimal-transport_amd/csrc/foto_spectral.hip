@@ -25,6 +25,22 @@ namespace foto {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Write-through 16-B stores (buffer_store_dwordx4 ... sc1): the line leaves the XCD's L2 at
+// once instead of staying dirty there.  A streaming kernel that ends with its L2s full of
+// dirty lines pays their write-back at the kernel boundary (MI355X_MICROARCH.md price list,
+// row "boundary": + B / 6 TB/s for B dirty bytes, up to 32 MiB here).  The resource covers
+// [base, base + 2^31 B); offsets are in bytes.
+#ifndef FOTO_PASS_WT
+#define FOTO_PASS_WT 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(double* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t rs, int off_bytes, dbl2 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off_bytes, 0, 16 /* sc1 */);
+}
 
 // ============================================================================ reductions (local copies)
 
@@ -1912,11 +1928,16 @@ __device__ __forceinline__ void vm_wait(int k) {
     }
 }
 
-// Usable for a shard when Nx is even (16-B lanes), the tables fit and the box's element
-// indices stay in 30 bits (32-bit tile and element arithmetic; ring_divmod's quotients, at
-// most Nt * nyl < 2^21 under the table bound, are exact).
+// Usable for a shard when Nx is even (16-B lanes) and the tables fit.  The flat tiling (Nx not
+// a multiple of 128) also needs the box's element indices in 30 bits (32-bit element
+// arithmetic; ring_divmod's quotients, at most Nt * nyl < 2^21 under the table bound, are
+// exact); row-segment tiles index with 64-bit element offsets; the write-through stores take
+// 32-bit byte offsets (a box under 4 GiB).
 static inline bool ring_ok(const SpecTab& T) {
-    return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB && (int64_t)T.Nt * T.nyl * T.Nx < (int64_t(1) << 30);
+    const bool flat = (T.Nx % 128) != 0;
+    return (T.Nx % 2) == 0 && T.Nx + T.Nt + T.nyl <= RING_TAB &&
+           (!flat || (int64_t)T.Nt * T.nyl * T.Nx < (int64_t(1) << 30)) &&
+           (!FOTO_PASS_WT || (int64_t)T.Nt * T.nyl * T.Nx * 8 < (int64_t(1) << 32));   // ring_store offsets
 }
 
 // Tables: mu_x [0, Nx), mu_t [Nx, Nx + Nt), mu_y of the own rows [Nx + Nt, + nyl).
@@ -1954,7 +1975,7 @@ __device__ __forceinline__ RingWave ring_wave(const SpecTab& T, double* ring, in
     const int rows = T.Nt * T.nyl;
     w.ntx = (T.Nx + 127) / 128;
     w.flat = (T.Nx % 128) != 0;
-    w.nel = rows * T.Nx;
+    w.nel = w.flat ? rows * T.Nx : 0;   // (< 2^30 when flat: ring_ok)
     const int nwt = w.flat ? (w.nel + 127) / 128 : rows * w.ntx;
     w.gw = blockIdx.x * RING_NW + wv;
     w.W = gridDim.x * RING_NW;
@@ -1963,39 +1984,91 @@ __device__ __forceinline__ RingWave ring_wave(const SpecTab& T, double* ring, in
     return w;
 }
 
-// DMA of tile j (r from src, q from ph when loadq) into its ring slot
-template <int D>
-__device__ __forceinline__ void ring_issue(const SpecTab& T, const RingWave& w, int j, const double* src,
-                                           const double* ph, bool loadq) {
-    const int lane = threadIdx.x & 63;
-    const int u = w.gw + j * w.W;
-    int64_t i;
-    if (w.flat) {
-        const int e = u * 128 + 2 * lane;
-        i = (e < w.nel) ? e : u * 128;   // idle lanes fetch a valid address; never read
-    } else {
-        const int row = u / w.ntx, cx = u - row * w.ntx;
-        int kx = cx * 128 + 2 * lane;
-        if (kx >= T.Nx) kx = cx * 128;
-        i = (int64_t)row * T.Nx + kx;
+// Wave-uniform position of a row-segment tile (Nx % 128 == 0): row = u / ntx, cx = u % ntx,
+// kt = row / nyl, ky = row % nyl, advanced by W tiles with scalar adds instead of the three
+// integer divisions per tile (~30 SALU instructions each) the loop used to spend.
+struct RingCursor {
+    int row, cx, kt, ky;
+    int dr, dc;   // W = dr * ntx + dc
+    __device__ __forceinline__ void init(int u, int W, int ntx, int nyl) {
+        row = u / ntx; cx = u - row * ntx;
+        kt = row / nyl; ky = row - kt * nyl;
+        dr = W / ntx; dc = W - dr * ntx;
     }
-    double* slot = w.wring + (j % D) * RING_SLOT;
+    __device__ __forceinline__ void step(int ntx, int nyl) {
+        cx += dc;
+        int d = dr;
+        if (cx >= ntx) { cx -= ntx; ++d; }
+        row += d;
+        ky += d;
+        while (ky >= nyl) { ky -= nyl; ++kt; }
+    }
+};
+
+// DMA of a tile (r from src, q from ph when loadq) into ring slot `slot`; i: the element of
+// this lane's first value (16 B per lane)
+__device__ __forceinline__ void ring_dma(double* slot, int64_t i, const double* src, const double* ph, bool loadq) {
     __builtin_amdgcn_global_load_lds((const void*)(src + i), (lds_void_t*)slot, 16, 0, 0);
     if (loadq) __builtin_amdgcn_global_load_lds((const void*)(ph + i), (lds_void_t*)(slot + 128), 16, 0, 0);
 }
 
-// One pass over the wave's tiles: apply the planned steps of S0 (none for INIT), write r (and
-// q), accumulate the moments of the new state into acc.  issued: tiles [0, issued) already
+// element index of this lane's pair in tile u (flat: idle lanes fetch a valid address, never read)
+template <bool FLAT>
+__device__ __forceinline__ int64_t ring_elem(const SpecTab& T, const RingWave& w, int u, int row, int cx) {
+    const int lane = threadIdx.x & 63;
+    if (FLAT) {
+        const int e = u * 128 + 2 * lane;
+        return (e < w.nel) ? e : u * 128;
+    }
+    return (int64_t)row * T.Nx + cx * 128 + 2 * lane;
+}
+
+// DMA of the wave's tile j (prologue issue outside the pass loop: the late-planning prefetch)
+template <int D>
+__device__ __forceinline__ void ring_issue(const SpecTab& T, const RingWave& w, int j, const double* src,
+                                           const double* ph, bool loadq) {
+    const int u = w.gw + j * w.W;
+    int64_t i;
+    if (w.flat) {
+        i = ring_elem<true>(T, w, u, 0, 0);
+    } else {
+        const int row = u / w.ntx;
+        i = ring_elem<false>(T, w, u, row, u - row * w.ntx);
+    }
+    ring_dma(w.wring + (j % D) * RING_SLOT, i, src, ph, loadq);
+}
+
+// 16-B store of r or q: write-through (sc1) when FOTO_PASS_WT (see st_wt16); the s_nop covers
+// the store-data hazard of a >8-B store before a later VALU write of its data registers
+// (inline asm is outside the compiler's hazard tracking)
+// (saddr form: the base in SGPRs and a 32-bit byte offset per lane, as the compiler's own stores;
+// a 64-bit address per lane cost the tile loop 4 VGPRs and spilled it)
+__device__ __forceinline__ void ring_store(double* base, int64_t i, dbl2 v) {
+#if FOTO_PASS_WT
+    const unsigned off = (unsigned)(i * 8);
+    asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" ::"v"(off), "v"(v), "s"(base) : "memory");
+#else
+    *reinterpret_cast<dbl2*>(base + i) = v;
+#endif
+}
+
+// One pass over the wave's tiles with S0's planned steps (none for INIT): apply them, write r
+// (and q), accumulate the moments of the new state into acc.  issued: tiles [0, issued) already
 // have their DMAs in flight or landed (a prefetch), the rest of the prologue is issued here.
-template <int D, bool INIT>
-__device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, unsigned tab_a, const SStep& S0,
-                                          double* __restrict__ rh, double* __restrict__ ph,
-                                          const double* __restrict__ bh, double (&acc)[NACC], int issued,
-                                          bool mom = true) {
+// FLAT is compile-time, so the row-segment loop has no tiling branches and no lane masks.
+template <int D, bool INIT, bool FLAT>
+__device__ __forceinline__ void ring_pass_t(const SpecTab& T, const RingWave& w, unsigned tab_a, const SStep& S0,
+                                            double* __restrict__ rh, double* __restrict__ ph,
+                                            const double* __restrict__ bh, double (&acc)[NACC], int issued, bool mom) {
     const int lane = threadIdx.x & 63;
     const int k = S0.k, ns = INIT ? 0 : S0.nsteps;
-    const double c0 = INIT ? S0.ic0 : S0.c0, ic1 = 1.0 / (INIT ? S0.ic1 : S0.c1);
-    const bool loadq = !INIT && k > 0;
+    // (the division runs on the VALU: readlane puts c0, 1 / c1 back in SGPRs, not in two VGPR
+    // pairs the register-bound loop would spill)
+    const double c0 = dbl_readlane(INIT ? S0.ic0 : S0.c0, 0), ic1 = dbl_readlane(1.0 / (INIT ? S0.ic1 : S0.c1), 0);
+    // wave-uniform flags as readfirstlane'd ints: a bool the compiler keeps as a lane mask turns
+    // the count switch and the q DMA into exec-masked (divergent) code
+    const bool loadq = __builtin_amdgcn_readfirstlane((!INIT && k > 0) ? 1 : 0) != 0;
+    const bool momu = __builtin_amdgcn_readfirstlane(mom ? 1 : 0) != 0;
     const double* src = (INIT || k == 0) ? bh : rh;   // r_0 = b^ (the INIT pass leaves it there)
     auto moments = [&](double lam, double r, double q) {
         const double x = (lam - c0) * ic1, x2 = x + x;
@@ -2019,38 +2092,52 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
     };
     const int nj = w.nj;
     const float invx = 1.0f / (float)T.Nx, invy = 1.0f / (float)T.nyl;
-    const int g = loadq ? 2 : 1;             // DMA instructions per tile
-    constexpr int NS = INIT ? 1 : 2;         // store instructions per tile
-    for (int j = issued; j < D - 1 && j < nj; ++j) ring_issue<D>(T, w, j, src, ph, loadq);
+    const int g = loadq ? 2 : 1;               // DMA instructions per tile
+    constexpr int NST = INIT ? 1 : 2;          // store instructions per tile
+    RingCursor cp{}, ci{};                     // the tile being processed / the next DMA's tile
+    if (!FLAT) {
+        cp.init(w.gw, w.W, w.ntx, T.nyl);
+        ci.init(w.gw + issued * w.W, w.W, w.ntx, T.nyl);
+    }
+    for (int j = issued; j < D - 1 && j < nj; ++j) {
+        ring_dma(w.wring + (j % D) * RING_SLOT, ring_elem<FLAT>(T, w, w.gw + j * w.W, ci.row, ci.cx), src, ph, loadq);
+        if (!FLAT) ci.step(w.ntx, T.nyl);
+    }
+    if (!FLAT && issued > D - 1) {   // (a prefetch never issues more than the prologue)
+        ci.init(w.gw + (D - 1) * w.W, w.W, w.ntx, T.nyl);
+    }
     for (int j = 0; j < nj; ++j) {
-        if (j + D - 1 < nj) ring_issue<D>(T, w, j + D - 1, src, ph, loadq);
+        if (j + D - 1 < nj) {
+            ring_dma(w.wring + ((j + D - 1) % D) * RING_SLOT,
+                     ring_elem<FLAT>(T, w, w.gw + (j + D - 1) * w.W, ci.row, ci.cx), src, ph, loadq);
+            if (!FLAT) ci.step(w.ntx, T.nyl);
+        }
         const int nG = min(j + D - 1, nj - 1) - j, nS = min(j, D - 1);
         // steady state (D - 1 tiles ahead and behind) as one immediate wait; the switch over
         // counts (a branch tree) only in the prologue and drain
         if (nG == D - 1 && nS == D - 1) {
-            if (INIT || !loadq) vm_wait_imm<(1 + NS) * (D - 1)>();
-            else vm_wait_imm<(2 + NS) * (D - 1)>();
+            if (INIT || !loadq) vm_wait_imm<(1 + NST) * (D - 1)>();
+            else vm_wait_imm<(2 + NST) * (D - 1)>();
         } else {
-            vm_wait(g * nG + NS * nS);
+            vm_wait(__builtin_amdgcn_readfirstlane(g * nG + NST * nS));
         }
         const int u = w.gw + j * w.W;
         int kx, kt, ky;
-        bool ok;
+        bool ok = true;
         int64_t i;
-        if (w.flat) {   // per lane: element e -> (row, kx) -> (kt, ky)
+        if (FLAT) {   // per lane: element e -> (row, kx) -> (kt, ky)
             const int e0 = u * 128 + 2 * lane;
             ok = e0 < w.nel;
             const int e = ok ? e0 : u * 128;
             const int row = ring_divmod(e, T.Nx, invx, &kx);
             kt = ring_divmod(row, T.nyl, invy, &ky);
             i = e;
-        } else {
-            const int row = u / w.ntx, cx = u - row * w.ntx;
-            kx = cx * 128 + 2 * lane;
-            kt = row / T.nyl;
-            ky = row - kt * T.nyl;
-            ok = kx < T.Nx;
-            i = (int64_t)row * T.Nx + kx;
+        } else {      // whole row segments: every lane valid
+            kx = cp.cx * 128 + 2 * lane;
+            kt = cp.kt;
+            ky = cp.ky;
+            i = (int64_t)cp.row * T.Nx + kx;
+            cp.step(w.ntx, T.nyl);
         }
         const unsigned sa = lds_u32(w.wring + (j % D) * RING_SLOT) + 16 * lane;
         dbl2 rv = lds_ld128(sa);
@@ -2064,16 +2151,17 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
         const double l0 = T.reps + T.r * (rowmu + mxv[0]);
         const double l1 = T.reps + T.r * (rowmu + mxv[1]);
         double r0 = rv[0], r1 = rv[1], q0 = qv[0], q1 = qv[1];
-        if (INIT) {
-            if (ok) *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
-        } else {
-            // fully unrolled with a guard (not a break): a rolled loop would index S0.a / S0.b
-            // dynamically and put S0 in scratch (measured: 3x slower pass at SMAX 10)
+        if (!INIT) {
+            // fully unrolled with a guard, not a break (a break leaves a rolled loop that indexes
+            // S0.a / S0.b from scratch with a divergent exit and a vmcnt(0) wait; measured 3x
+            // slower at SMAX 10)
 #pragma clang loop unroll(full)
             for (int st = 0; st < SMAX; ++st) {
                 if (st < ns) {
+                    // iteration k + st: p = beta p + r (k + st = 0: b = 0, q = 0, so p = r);
+                    // r -= alpha (lam p)
                     const double a = S0.a[st], b = S0.b[st];
-                    const double p0 = fma(b, q0, r0);   // k + st = 0: b = 0, q = 0 (p = r)
+                    const double p0 = fma(b, q0, r0);
                     const double p1 = fma(b, q1, r1);
                     r0 = fma(-a, l0 * p0, r0);
                     r1 = fma(-a, l1 * p1, r1);
@@ -2081,12 +2169,14 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
                     q1 = p1;
                 }
             }
-            if (ok) {
-                *reinterpret_cast<dbl2*>(rh + i) = dbl2{r0, r1};
-                *reinterpret_cast<dbl2*>(ph + i) = dbl2{q0, q1};
-            }
         }
-        if (ok && mom) {
+        if (ok) {
+            ring_store(rh, i, dbl2{r0, r1});
+            if (!INIT) ring_store(ph, i, dbl2{q0, q1});
+        }
+        if (momu) {
+            // idle lanes of a flat tail contribute exact zeros (r = q = 0: fma(t, 0, acc) = acc)
+            if (!ok) r0 = r1 = q0 = q1 = 0.0;
 #if defined(FOTO_RING_ABLATE)   // timing studies only (tools/pass_lab.hip): no moments
             acc[0] += r0 * q0 + r1 * q1 + l0 * l1;
 #else
@@ -2095,6 +2185,17 @@ __device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, u
 #endif
         }
     }
+}
+
+// The pass over the wave's tiles with S0's planned steps (dispatch on the tiling; per element the
+// arithmetic is the register-fed pass's, in the same order).
+template <int D, bool INIT>
+__device__ __forceinline__ void ring_pass(const SpecTab& T, const RingWave& w, unsigned tab_a, const SStep& S0,
+                                          double* __restrict__ rh, double* __restrict__ ph,
+                                          const double* __restrict__ bh, double (&acc)[NACC], int issued,
+                                          bool mom = true) {
+    if (w.flat) ring_pass_t<D, INIT, true>(T, w, tab_a, S0, rh, ph, bh, acc, issued, mom);
+    else ring_pass_t<D, INIT, false>(T, w, tab_a, S0, rh, ph, bh, acc, issued, mom);
 }
 
 // SStep from LDS into wave-uniform registers (the plan made in LDS feeds the step loop's
@@ -2132,6 +2233,10 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
     // state's, so the two round trips overlap instead of running back to back (the plan waits
     // for both).  The asm use pins the loads above the state checks.
     __shared__ double tot[NACC];
+    // the state the tail publishes: the plan made at the start (late) or the one in Sg; kept in
+    // LDS so the tile loop holds only the fields it uses in registers (the whole SStep live
+    // across the loop cost SGPR spills -- v_readlane reloads in every tile)
+    __shared__ SStep Sl;
     double gpre = 0.0;
     if (LATE && threadIdx.x < NACC) gpre = gath[threadIdx.x];   // rank 0's slot
     SStep S0 = *Sg;
@@ -2147,7 +2252,6 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
             // Wave 0 plans at once: the previous pass's moments into LDS (its own lanes, so a
             // wave-local wait orders them), its first tiles issued behind them, the plan.  The
             // other waves stage the tables and issue their first tiles meanwhile.
-            __shared__ SStep Sl;
             const int k = S0.k + S0.nsteps;
             const double* src = (k == 0) ? bh : rh;
             if (!S0.fin) issued = min(D - 1, w.nj);   // the plan will apply steps
@@ -2183,6 +2287,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
             }
 #endif
         } else {
+            if (threadIdx.x == 0) Sl = S0;
             ring_stage_tables(T, tab);
             __syncthreads();
         }
@@ -2203,7 +2308,7 @@ __global__ __launch_bounds__(S2_NTH) __attribute__((amdgpu_waves_per_eu(S2_WPE))
         if (!S0.done && !final_pass)   // this rank's slot (the all-gather between passes fills the others)
             for (int m = threadIdx.x; m < NACC; m += S2_NTH) gath[rank * NACC + m] = tot[m];
         if (threadIdx.x == 0) {
-            SStep So = S0;
+            SStep So = Sl;   // == S0 (thread 0 wrote it before the barrier)
             if (final_pass) {
                 So.k += So.nsteps;
                 So.done = So.conv ? 1 : 2;
@@ -3089,5 +3194,75 @@ extern "C" int foto_dct(const double* in, int outer, int n, int inner, int inver
     (void)hipStreamSynchronize(s);
     for (void* p : bufs) (void)hipFree(p);
     (void)hipStreamDestroy(s);
+    return rc;
+}
+
+// ============================================================================ C ABI: stream ceiling probe
+// The s-step pass's memory traffic alone -- read r, q (16 B per lane), write r, q -- with no
+// moments, no plan and no reduction: what the dominant kernel could reach on this device.
+// bench.py reports the pass against it (roofline.stream_frac) beside the HBM-peak fraction,
+// because the pass's 157 MB working set sits in the 256 MiB Infinity Cache.
+
+namespace foto {
+template <bool WT>
+__global__ __launch_bounds__(256) void k_stream_rq(double* __restrict__ r, double* __restrict__ q, int64_t n2,
+                                                   double a, double b) {
+    const __amdgpu_buffer_rsrc_t rr = wt_rsrc(r), rq = wt_rsrc(q);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+        const dbl2 rv = reinterpret_cast<const dbl2*>(r)[i], qv = reinterpret_cast<const dbl2*>(q)[i];
+        const dbl2 pn = b * qv + rv, rn = rv - a * pn;
+        if (WT) {
+            st_wt16(rr, (int)(i * 16), rn);
+            st_wt16(rq, (int)(i * 16), pn);
+        } else {
+            reinterpret_cast<dbl2*>(r)[i] = rn;
+            reinterpret_cast<dbl2*>(q)[i] = pn;
+        }
+    }
+}
+}  // namespace foto
+
+extern "C" int foto_stream_probe(int64_t n, int reps, double* us) {
+    using namespace foto;
+    if (!us || n < 2 || n % 2 || reps < 1 || n * 8 >= (int64_t(1) << 31)) {
+        set_error("foto_stream_probe: bad arguments (n even, n * 8 < 2^31)");
+        return FOTO_ERR_ARG;
+    }
+    hipStream_t s = nullptr;
+    double *r = nullptr, *q = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto body = [&]() -> int {
+        FOTO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        FOTO_HIP_CHECK(hipMalloc((void**)&r, n * 8));
+        FOTO_HIP_CHECK(hipMalloc((void**)&q, n * 8));
+        FOTO_HIP_CHECK(hipMemsetAsync(r, 0, n * 8, s));
+        FOTO_HIP_CHECK(hipMemsetAsync(q, 0, n * 8, s));
+        FOTO_HIP_CHECK(hipEventCreate(&e0));
+        FOTO_HIP_CHECK(hipEventCreate(&e1));
+        for (int wt = 0; wt < 2; ++wt) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 3; ++rep) {
+                FOTO_HIP_CHECK(hipEventRecord(e0, s));
+                for (int k = 0; k < reps; ++k) {
+                    if (wt) k_stream_rq<true><<<1024, 256, 0, s>>>(r, q, n / 2, 1e-9, 1e-9);
+                    else k_stream_rq<false><<<1024, 256, 0, s>>>(r, q, n / 2, 1e-9, 1e-9);
+                }
+                FOTO_HIP_CHECK(hipGetLastError());
+                FOTO_HIP_CHECK(hipEventRecord(e1, s));
+                FOTO_HIP_CHECK(hipEventSynchronize(e1));
+                float t = 0.f;
+                FOTO_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+                best = std::min(best, t);
+            }
+            us[wt] = 1e3 * best / reps;
+        }
+        return 0;
+    };
+    const int rc = body();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (r) (void)hipFree(r);
+    if (q) (void)hipFree(q);
+    if (s) (void)hipStreamDestroy(s);
     return rc;
 }

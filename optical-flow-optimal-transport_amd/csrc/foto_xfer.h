@@ -1,0 +1,112 @@
+// Transfer lists of the time-sharded Benamou-Brenier solve (host-only C++, no HIP).
+//
+// Every exchange between the shards of the 8-GPU decomposition (contiguous
+// time slabs, benamou_brenier.py:204-258 sharded on t) is a list of point-to-point transfers
+// {src rank, dst rank, src offset, dst offset, count}, built by the same code on every rank.
+// foto_bb.cpp executes a list either as device copies (virtual ranks, one process) or as one
+// RCCL group (ncclSend for each transfer from this rank, ncclRecv for each transfer to it,
+// in list order; a transfer to itself is a device copy).  rccl_calls() is that issue order,
+// and the test entry foto_xfer_calls (foto_bb.cpp) exposes it so a CPU test can check that
+// every rank's sends pair with its peers' receives for W = 2 .. 8 without a GPU.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+namespace foto {
+
+// balanced split of n items over W ranks: rank gets [*t0, *t0 + *nloc)
+inline int split_planes(int n, int W, int rank, int* t0, int* nloc) {
+    const int base = n / W, extra = n % W;
+    *nloc = base + (rank < extra ? 1 : 0);
+    *t0 = rank * base + std::min(rank, extra);
+    return *nloc >= 1 ? 0 : -1;
+}
+
+struct Xfer {
+    int src, dst;
+    int64_t soff, doff, n;   // doubles, relative to the picked buffer of each shard
+};
+
+// halo planes of a halo-padded field (pointer at local plane 0): plane -1 <- the previous
+// rank's last plane, plane nloc <- the next rank's first plane
+inline std::vector<Xfer> halo_xfers(int Nt, int64_t nxy, int W) {
+    std::vector<Xfer> xs;
+    for (int j = 0; j + 1 < W; ++j) {
+        int t0, nl;
+        split_planes(Nt, W, j, &t0, &nl);
+        xs.push_back({j, j + 1, (int64_t)(nl - 1) * nxy, -nxy, nxy});   // up: last plane -> halo below
+        xs.push_back({j + 1, j, 0, (int64_t)nl * nxy, nxy});             // down: first plane -> halo above
+    }
+    return xs;
+}
+
+// all-to-all between the physical slabs and the spectral row boxes (SpectralPlan):
+//   forward : rank a sends stage_a[na*Nx*y0_b, + na*nyl_b*Nx]   -> box_in_b[t0_a*nyl_b*Nx, ...]
+//   backward: rank a sends box_out_a[t0_b*nyl_a*Nx, + nb*nyl_a*Nx] -> stage_b[nb*Nx*y0_a, ...]
+inline std::vector<Xfer> alltoall_xfers(int Nt, int Ny, int Nx, int W, bool forward) {
+    std::vector<Xfer> xs;
+    for (int a = 0; a < W; ++a)
+        for (int b = 0; b < W; ++b) {
+            int ta, na, tb, nb, ya, nya, yb, nyb;
+            split_planes(Nt, W, a, &ta, &na);
+            split_planes(Nt, W, b, &tb, &nb);
+            split_planes(Ny, W, a, &ya, &nya);
+            split_planes(Ny, W, b, &yb, &nyb);
+            int64_t so, ro, n;
+            if (forward) {
+                so = (int64_t)na * Nx * yb; n = (int64_t)na * nyb * Nx; ro = (int64_t)ta * nyb * Nx;
+            } else {
+                so = (int64_t)tb * nya * Nx; n = (int64_t)nb * nya * Nx; ro = (int64_t)nb * Nx * ya;
+            }
+            if (n > 0) xs.push_back({a, b, so, ro, n});
+        }
+    return xs;
+}
+
+// trajectory positions after rank j's planes -> rank j + 1 (one list per field, px and py)
+inline std::vector<Xfer> relay_xfers(int64_t nxy, int j) { return {{j, j + 1, 0, 0, nxy}}; }
+
+// the last rank's (u, v, m) -> rank 0 (one list per field)
+inline std::vector<Xfer> deliver_xfers(int64_t nxy, int W) { return {{W - 1, 0, 0, 0, nxy}}; }
+
+// in-place all-gather of `cnt` doubles per rank, as device copies (virtual ranks; RCCL runs
+// one ncclAllGather instead)
+inline std::vector<Xfer> allgather_xfers(int W, int cnt) {
+    std::vector<Xfer> xs;
+    for (int g = 0; g < W; ++g)
+        for (int h = 0; h < W; ++h)
+            if (g != h) xs.push_back({g, h, (int64_t)g * cnt, (int64_t)g * cnt, cnt});
+    return xs;
+}
+
+// What rank `me` issues for a list over RCCL, in issue order: inside one group (when any
+// transfer crosses ranks) a send for each transfer from `me` to a peer and a receive for each
+// transfer from a peer to `me`, in list order; after the group, each transfer to itself as a
+// device copy.
+enum CallOp { CALL_SEND = 0, CALL_RECV = 1, CALL_COPY = 2 };
+struct Call {
+    int op, peer;
+    int64_t off, n, doff;   // send / copy: source offset; recv: destination offset; copy: doff too
+};
+
+inline bool crosses_ranks(const std::vector<Xfer>& xs, int me) {
+    for (const Xfer& x : xs)
+        if ((x.src == me) != (x.dst == me)) return true;
+    return false;
+}
+
+inline std::vector<Call> rccl_calls(const std::vector<Xfer>& xs, int me) {
+    std::vector<Call> cs;
+    if (crosses_ranks(xs, me))
+        for (const Xfer& x : xs) {
+            if (x.src == me && x.dst != me) cs.push_back({CALL_SEND, x.dst, x.soff, x.n, 0});
+            if (x.dst == me && x.src != me) cs.push_back({CALL_RECV, x.src, x.doff, x.n, 0});
+        }
+    for (const Xfer& x : xs)
+        if (x.src == me && x.dst == me) cs.push_back({CALL_COPY, me, x.soff, x.n, x.doff});
+    return cs;
+}
+
+}  // namespace foto

@@ -93,7 +93,9 @@ SIGNATURES = {
     "foto_bb_destroy": (None, [_P]),
     "foto_bb_solve": (_I, [_D, _D, _I, _I, _I, _Dbl, _Dbl, _Dbl, _I, ITER_CB, _P, _D, _D, _D]),
     "foto_nccl_unique_id": (_I, [_P]),
+    "foto_xfer_calls": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_int64), _I, ctypes.POINTER(_I)]),
     "foto_dct": (_I, [_D, _I, _I, _I, _I, _I, _D]),
+    "foto_stream_probe": (_I, [ctypes.c_int64, _I, _D]),
     "foto_gn_apply": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _D, _D]),
     "foto_gn_rhs": (_I, [_D, _D, _I, _I, _D]),
     "foto_gn_solve": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _Dbl, _I, _D, _D, _D, ctypes.POINTER(_I)]),
@@ -110,25 +112,31 @@ SIGNATURES = {
 _lib = None
 
 
+def load(path):
+    """A libfoto build at `path` with every signature of include/foto.h set (lib() is the
+    product library; tests load libfoto_mockrccl.so, the in-process RCCL transport, this way)."""
+    if not os.path.exists(path):
+        raise FotoError(f"libfoto.so not found at {path}; build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C csrc`")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
     """Load libfoto.so (once).  Raises if it is missing: there is no CPU fallback."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise FotoError(f"libfoto.so not found at {LIB_PATH}; build it with "
-                            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C csrc`")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
 
 
-def check(rc):
+def check(rc, L=None):
     if rc < 0:
-        msg = lib().foto_last_error().decode(errors="replace")
+        msg = (L or lib()).foto_last_error().decode(errors="replace")
         if rc == FOTO_ERR_BC:
             raise NotImplementedError("These boundary conditions are not implemented")
         raise FotoError(f"libfoto error {rc}: {msg}")

@@ -25,12 +25,14 @@ class BBSolver:
     2 = that spectral CG in s-step passes of up to 8 iterations -- the default, as in the C
     ABI's foto_bb_opts_default and the drop-in benamou_brenier.solve);
     ``rank/world/nccl_id`` shard the time axis over processes (RCCL),
-    ``virtual_ranks`` shards it in-process on one device (test path).
+    ``virtual_ranks`` shards it in-process on one device (test path); ``library`` is a
+    ``_lib.load``-ed build other than the product libfoto.so (tests).
     """
 
     def __init__(self, rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-3, *, device=-1, cg_rtol=1e-6,
                  cg_maxiter=1000, cg_mode=CG_SSTEP, rank=0, world=1, nccl_id=None, virtual_ranks=1,
-                 timing=False):
+                 timing=False, library=None):
+        self._L = library if library is not None else lib()
         Nt, Nx, Ny = int(Nt), int(Nx), int(Ny)
         if Nt < 2:
             raise ZeroDivisionError("Nt must be >= 2 (benamou_brenier.py:194 divides by Nt - 1)")
@@ -41,7 +43,7 @@ class BBSolver:
         self._rho0 = f64(rho0, nxy, "rho0")
         self._rhoT = f64(rhoT, nxy, "rhoT")
         o = _lib.BBOpts()
-        lib().foto_bb_opts_default(ctypes.byref(o))
+        self._L.foto_bb_opts_default(ctypes.byref(o))
         o.device = int(device)
         o.cg_rtol = float(cg_rtol)
         o.cg_maxiter = int(cg_maxiter)
@@ -55,7 +57,7 @@ class BBSolver:
         o.virtual_ranks = int(virtual_ranks)
         o.timing = 1 if timing else 0
         self._ctx = ctypes.c_void_p()
-        check(lib().foto_bb_create(dptr(self._rho0), dptr(self._rhoT), Nt, Nx, Ny, self.r, self.eps,
+        self._check(self._L.foto_bb_create(dptr(self._rho0), dptr(self._rhoT), Nt, Nx, Ny, self.r, self.eps,
                                    ctypes.byref(o), ctypes.byref(self._ctx)))
         self.world = int(world)
         self.rank = int(rank)
@@ -63,10 +65,13 @@ class BBSolver:
         self.cg_its = []
         self.cg_info = []
 
+    def _check(self, rc):
+        return check(rc, self._L)
+
     # -------------------------------------------------------------- lifecycle
     def close(self):
         if getattr(self, "_ctx", None) and self._ctx.value:
-            lib().foto_bb_destroy(self._ctx)
+            self._L.foto_bb_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
 
     def __del__(self):
@@ -99,35 +104,35 @@ class BBSolver:
 
         cb = _lib.ITER_CB(_cb)
         done = ctypes.c_int(0)
-        rc = lib().foto_bb_iterate(self._ctx, int(n), float(convergence_tol), 1 if stop_rules else 0, cb, None,
+        rc = self._L.foto_bb_iterate(self._ctx, int(n), float(convergence_tol), 1 if stop_rules else 0, cb, None,
                                    ctypes.byref(done))
         if errors:
             raise errors[0]
-        check(rc)
+        self._check(rc)
         return rc == 1
 
     def flow(self):
         """(u, v, m) from the last phi (rank 0 gets the arrays; other ranks get None)."""
         nxy = self.Nx * self.Ny
         if self.world > 1 and self.rank != 0:
-            check(lib().foto_bb_flow(self._ctx, None, None, None))
+            self._check(self._L.foto_bb_flow(self._ctx, None, None, None))
             return None
         u = np.empty(nxy)
         v = np.empty(nxy)
         m = np.empty(nxy)
-        check(lib().foto_bb_flow(self._ctx, dptr(u), dptr(v), dptr(m)))
+        self._check(self._L.foto_bb_flow(self._ctx, dptr(u), dptr(v), dptr(m)))
         return u, v, m
 
     def shard(self):
         t0 = ctypes.c_int()
         nl = ctypes.c_int()
-        check(lib().foto_bb_shard(self._ctx, ctypes.byref(t0), ctypes.byref(nl)))
+        self._check(self._L.foto_bb_shard(self._ctx, ctypes.byref(t0), ctypes.byref(nl)))
         return t0.value, nl.value
 
     def phi(self):
         _, nl = self.shard()
         out = np.empty(nl * self.Nx * self.Ny)
-        check(lib().foto_bb_get_phi(self._ctx, dptr(out)))
+        self._check(self._L.foto_bb_get_phi(self._ctx, dptr(out)))
         return out
 
     def state(self):
@@ -135,12 +140,12 @@ class BBSolver:
         n = nl * self.Nx * self.Ny
         mu = np.empty(3 * n)
         q = np.empty(3 * n)
-        check(lib().foto_bb_get_state(self._ctx, dptr(mu), dptr(q)))
+        self._check(self._L.foto_bb_get_state(self._ctx, dptr(mu), dptr(q)))
         return mu, q
 
     def stats(self):
         st = _lib.BBStats()
-        check(lib().foto_bb_stats_get(self._ctx, ctypes.byref(st)))
+        self._check(self._L.foto_bb_stats_get(self._ctx, ctypes.byref(st)))
         d = {f: getattr(st, f) for f in ("outer_iters", "cg_iters_total", "last_crit", "ms_rhs", "ms_cg",
                                          "ms_prox", "ms_flow", "cg_redo")}
         d["kernels"] = {name: {"n": int(st.n_k[i]), "ms": float(st.ms_k[i]), "bytes": float(st.bytes_k[i])}
@@ -148,13 +153,13 @@ class BBSolver:
         return d
 
     def reset_stats(self):
-        check(lib().foto_bb_stats_reset(self._ctx))
+        self._check(self._L.foto_bb_stats_reset(self._ctx))
 
     def set_timing(self, on):
-        check(lib().foto_bb_set_timing(self._ctx, 1 if on else 0))
+        self._check(self._L.foto_bb_set_timing(self._ctx, 1 if on else 0))
 
     def sync(self):
-        check(lib().foto_bb_sync(self._ctx))
+        self._check(self._L.foto_bb_sync(self._ctx))
 
 
 def solve(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, max_it=100, *, log=print,

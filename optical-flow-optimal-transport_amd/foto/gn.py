@@ -1,5 +1,7 @@
 """Gennert-Negahdaripour baseline on the GPU (classical.py:25-130 semantics)."""
+import collections
 import ctypes
+import sys
 
 import numpy as np
 
@@ -76,7 +78,35 @@ class Plan:
         self.close()
 
     def __del__(self):
+        # at interpreter shutdown the HIP runtime may already be torn down: leave the plan
+        # to process exit (foto_capi.cpp's cached plan does the same)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
             pass
+
+
+PLAN_CACHE_SIZE = 4
+_plans = collections.OrderedDict()
+
+
+def cached_plan(w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
+    """A process-wide Plan for (w, h, alpha, lambda, rtol, maxiter), shared by every
+    GLLOpticalFlow instance (least recently used of PLAN_CACHE_SIZE dropped): a batch of frames
+    of one size -- run.sh's per-sequence GN runs -- makes its buffers, multigrid hierarchy and
+    graph once, and instances that come and go do not each hold device memory."""
+    key = (int(w), int(h), float(alpha), float(lam), float(rtol), int(maxiter))
+    p = _plans.pop(key, None)
+    if p is None:
+        p = Plan(*key)
+        while len(_plans) >= PLAN_CACHE_SIZE:
+            _plans.popitem(last=False)[1].close()
+    _plans[key] = p
+    return p
+
+
+def clear_plan_cache():
+    while _plans:
+        _plans.popitem()[1].close()

@@ -307,8 +307,9 @@ def test_bb_fused_prox_rhs_matches_separate(gold, monkeypatch, name, mode):
     (k_prox_rhs: F from the new mu, q of a tile plus a one-voxel ring; q never stored).  Its
     per-voxel arithmetic is k_prox's and k_rhs's in the same order, so against the separate
     kernels (FOTO_FUSE_PR=0) mu, phi, q (recomputed by state()) and the flow are bit-identical;
-    only the crit sums are grouped differently (1e-14).  Chunk sizes 1, 3 and the default 8
-    (planes per block) cover the chunk seams and the t = 0 / Nt - 1 boundary terms."""
+    only the crit sums are grouped differently (1e-14).  These goldens have Nt <= 8, one chunk
+    at the default 16 planes per block; test_bb_fused_prox_rhs_chunks covers the chunk seams
+    (1 and 3 planes, and the default 16 on a 20-plane grid) and the t = 0 / Nt - 1 terms."""
     d = gold(name)
     Nt, Ny, Nx = (int(v) for v in d["shape"])
     r, _, eps, _ = d["params"]
@@ -333,21 +334,38 @@ def test_bb_fused_prox_rhs_matches_separate(gold, monkeypatch, name, mode):
             np.testing.assert_allclose(y, x, rtol=0, atol=1e-10 * max(np.abs(x).max(), 1e-300))
 
 
-@pytest.mark.parametrize("tch", ["1", "3"])
-def test_bb_fused_prox_rhs_chunks(gold, monkeypatch, tch):
-    d = gold("bb_tex.npz")
-    Nt, Ny, Nx = (int(v) for v in d["shape"])
-    r, _, eps, _ = d["params"]
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("tch", ["1", "3", "default"])
+def test_bb_fused_prox_rhs_chunks(gold, monkeypatch, tch, mode):
+    """Chunk seams of the k_prox_rhs t-march: 1 and 3 planes per chunk on the textured golden
+    (Nt = 5), and the default 16 on a 20-plane grid (one seam at t = 16), in the spectral and
+    the stencil CG modes: mu, q and phi bit-identical to the separate k_prox / k_rhs."""
+    if tch == "default":
+        from foto.synthetic import translating_gaussian
+        Nt, Ny, Nx, r, eps = 20, 30, 40, 1.0, 1e-2
+        rho0, rhoT = translating_gaussian(Nx, Ny)
+    else:
+        d = gold("bb_tex.npz")
+        Nt, Ny, Nx = (int(v) for v in d["shape"])
+        r, _, eps, _ = d["params"]
+        rho0, rhoT = d["rho0"], d["rhoT"]
     out = []
-    for env in ({"FOTO_FUSE_PR": "0"}, {"FOTO_FUSE_PR": "1", "FOTO_PR_TCH": tch}):
+    fused = {"FOTO_FUSE_PR": "1"} if tch == "default" else {"FOTO_FUSE_PR": "1", "FOTO_PR_TCH": tch}
+    for env in ({"FOTO_FUSE_PR": "0"}, fused):
+        monkeypatch.delenv("FOTO_PR_TCH", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
             s.iterate(3, 0.0, False)
-            out.append((s.state(), s.phi()))
-    (mu0, q0), p0 = out[0]
-    (mu1, q1), p1 = out[1]
-    assert np.array_equal(mu0, mu1) and np.array_equal(q0, q1) and np.array_equal(p0, p1)
+            out.append((s.state(), s.phi(), list(s.cg_its)))
+    (mu0, q0), p0, c0 = out[0]
+    (mu1, q1), p1, c1 = out[1]
+    assert c0 == c1
+    if mode == 2:
+        assert np.array_equal(mu0, mu1) and np.array_equal(q0, q1) and np.array_equal(p0, p1)
+    else:   # the stencil CG seeds rho_0 with F.F, summed in another order: CG rounding only
+        for x, y in ((mu0, mu1), (q0, q1), (p0, p1)):
+            np.testing.assert_allclose(y, x, rtol=0, atol=1e-10 * max(np.abs(x).max(), 1e-300))
 
 
 def test_bb_errors():

@@ -1,0 +1,122 @@
+"""The RCCL code path of the time-sharded solve, run on one GPU.
+
+bench.py --gpus N and the 8-GPU configs (BASELINE configs 4 and 5) shard the outer loop of
+benamou_brenier.py:204-258 over time slabs with one process per GPU; every exchange then goes
+through foto_bb.cpp's RCCL branches (grouped ncclSend / ncclRecv, the in-place ncclAllGather of
+the s-step moments).  Real RCCL refuses two ranks on one device and the test boxes have one GPU,
+so libfoto_mockrccl.so -- the same objects linked to an in-process transport with NCCL's
+matching rules (csrc/foto_mockrccl.cpp) -- runs W ranks as W threads on one device.
+
+The virtual-rank path (all shards in one context, the same transfer lists executed as device
+copies) is already checked against the single-GPU solve (test_gpu_parity.py).  Here each rank
+is its own context, exactly as in a multi-process run, and its results must be BIT-identical to
+the virtual ranks': the same kernels on the same slabs and boxes, the same moment sums in rank
+order, only the transport differs.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+MOCK = os.path.join(PKG, "foto", "libfoto_mockrccl.so")
+
+pytestmark = pytest.mark.gpu
+
+
+def _mock():
+    from foto import _lib
+    return _lib.load(MOCK)
+
+
+def run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters, cg_mode=2, eps=1e-2):
+    """W threads, one BBSolver (one RCCL-mode context) each; returns per-rank results."""
+    import ctypes
+    from foto import _lib
+    from foto.bb import BBSolver
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(L.foto_nccl_unique_id(buf), L)
+    nid = bytes(buf.raw)
+    out = [None] * W
+    errs = []
+
+    def rank(g):
+        try:
+            with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=eps, device=0, cg_mode=cg_mode, rank=g,
+                          world=W, nccl_id=nid, library=L) as s:
+                s.iterate(iters, 0.0, stop_rules=False)
+                fl = s.flow()
+                out[g] = {"crit": list(s.crit), "cg": list(s.cg_its), "flow": fl, "phi": s.phi(),
+                          "shard": s.shard(), "redo": s.stats()["cg_redo"]}
+        except BaseException as e:  # noqa: BLE001 -- reported by the main thread
+            errs.append((g, e))
+
+    th = [threading.Thread(target=rank, args=(g,)) for g in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung (mock RCCL waits are bounded: see the log)"
+    assert not errs, errs
+    return out
+
+
+def run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters, cg_mode=2, eps=1e-2):
+    from foto.bb import BBSolver
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=eps, device=0, cg_mode=cg_mode, virtual_ranks=W,
+                  library=L) as s:
+        s.iterate(iters, 0.0, stop_rules=False)
+        return {"crit": list(s.crit), "cg": list(s.cg_its), "flow": s.flow(), "phi": s.phi()}
+
+
+def compare(ranks, virt, Nt, Nx, Ny, W):
+    nxy = Nx * Ny
+    for g, res in enumerate(ranks):
+        assert res["crit"] == virt["crit"], (g, res["crit"][:3], virt["crit"][:3])
+        assert res["cg"] == virt["cg"], (g, res["cg"], virt["cg"])
+        t0, nl = res["shard"]
+        np.testing.assert_array_equal(res["phi"], virt["phi"][t0 * nxy:(t0 + nl) * nxy])
+    for a, b in zip(ranks[0]["flow"], virt["flow"]):
+        np.testing.assert_array_equal(a, b)
+    for g in range(1, W):
+        assert ranks[g]["flow"] is None
+
+
+@pytest.mark.parametrize("W", [2, 3, 5, 8])
+def test_rccl_path_bit_identical_to_virtual_ranks(W):
+    from foto.synthetic import translating_gaussian
+    Nt, Nx, Ny = 16, 64, 48
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+
+
+def test_rccl_path_stencil_cg():
+    """cg_mode 0: a halo exchange of p and two scalar all-gathers per CG iteration."""
+    from foto.synthetic import translating_gaussian
+    Nt, Nx, Ny, W = 9, 40, 30, 3
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=0)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=0)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+
+
+def test_rccl_path_bench_grid_w8():
+    """The driver's 8-GPU scaling run: the bench grid 640x480x32 over 8 ranks (4 planes and 60
+    rows each), three outer iterations, against the same decomposition as virtual ranks and,
+    within the spectral path's bar, against one shard."""
+    from foto.synthetic import translating_gaussian
+    Nt, Nx, Ny, W = 32, 640, 480, 8
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+    one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=3)
+    assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
+    np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)

@@ -1,5 +1,5 @@
 # Experiment (CPU, test infrastructure: imports the oracle and the numpy plan restatement).
-# usage: python tests/cs_bound_exp.py exact|cs 80x60x32 [limit]
+# usage: python tools/cs_bound_exp.py exact|cs 80x60x32 [limit]
 # Pass counts of the s-step plan with the exact |terms| cancellation ratio vs the Cauchy-Schwarz
 # bound (|H_ac| <= sqrt(H_aa H_cc)), on the first BB solve of a translating-Gaussian pair.
 import sys, math, time

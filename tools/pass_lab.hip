@@ -21,6 +21,18 @@ __global__ __launch_bounds__(256) void stream_rq(double* __restrict__ r, double*
     }
 }
 
+// the same stream with write-through (sc1) stores: no dirty L2 lines at the kernel boundary
+__global__ __launch_bounds__(256) void stream_rq_wt(double* __restrict__ r, double* __restrict__ q, size_t n2, double a,
+                                                    double b) {
+    const __amdgpu_buffer_rsrc_t rr = wt_rsrc(r), rq = wt_rsrc(q);
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += (size_t)gridDim.x * 256) {
+        dbl2 rv = ((const dbl2*)r)[i], qv = ((const dbl2*)q)[i];
+        dbl2 pn = b * qv + rv, rn = rv - a * pn;
+        st_wt16(rr, (int)(i * 16), rn);
+        st_wt16(rq, (int)(i * 16), pn);
+    }
+}
+
 
 // Kernel-boundary cost: npass ring passes in ONE launch (each block keeps its tiles and its
 // LDS tables across passes), optionally with a grid-wide arrival counter between passes (the
@@ -111,7 +123,7 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(Sg, &S0, sizeof(SStep), hipMemcpyHostToDevice);
         (void)hipMemcpy(Sg2, &S0, sizeof(SStep), hipMemcpyHostToDevice);
     };
-    printf("SMAX=%d S2_NTH=%d ring D=%d grid %dx%dx%d\n", SMAX, S2_NTH, FOTO_RING_D, Nx, Ny, Nt);
+    printf("SMAX=%d S2_NTH=%d ring D=%d pass sc1 stores %d grid %dx%dx%d\n", SMAX, S2_NTH, FOTO_RING_D, FOTO_PASS_WT, Nx, Ny, Nt);
     // correctness: one pass each from the same state, moments to gath (no fused plan)
     reset();
     const int G = 256;
@@ -157,6 +169,8 @@ int main(int argc, char** argv) {
     };
     timeit("pure stream r,q (1024 x 256)", [&] { stream_rq<<<1024, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
     timeit("pure stream r,q (2048 x 256)", [&] { stream_rq<<<2048, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
+    timeit("pure stream r,q, sc1 stores (1024 x 256)", [&] { stream_rq_wt<<<1024, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
+    timeit("pure stream r,q, sc1 stores (2048 x 256)", [&] { stream_rq_wt<<<2048, 256>>>(r, p, n / 2, 1e-9, 1e-9); });
     timeit("product k_spec_s2, moments only", [&] { k_spec_s2<true, false, false><<<256, S2_NTH>>>(T, r, p, b, Sg, rb, 1e-6, 1000, gath, 0); });
     for (int d : {2, 4, FOTO_RING_D}) {
         char nm[64];

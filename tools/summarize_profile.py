@@ -141,7 +141,12 @@ def main():
     json.dump({"kernel_stats": stats, "pmc": traffic}, open(os.path.join(a.out, f"{a.tag}_rocprof.json"), "w"),
               indent=1)
     if traffic:
-        json.dump(traffic, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
+        # "_source": the profile these per-launch bytes come from (bench.py quotes it as
+        # roofline.traffic_source: the traffic is measured by rocprofv3 PMC passes, not in the
+        # bench run itself)
+        src = {"_source": f"profiles/{a.tag}_rocprof_summary.md (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, "
+                          f"calibrated by tools/calib_fetch)"}
+        json.dump({**src, **traffic}, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
 
 
