@@ -322,7 +322,10 @@ def main():
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": dom, "alg_bytes_per_launch": k["bytes"] / k["n"], "avg_launch_us": round(avg_s * 1e6, 2)}
             if dom == "spec_cg":
-                roof.update(stream_ceiling(world, avg_s * 1e6))
+                try:
+                    roof.update(stream_ceiling(world, avg_s * 1e6))
+                except Exception as e:   # an older library in an A/B run (FOTO_LIB) has no probe
+                    roof["stream_note"] = f"stream probe unavailable: {e}"
 
     line = None
     if rank == 0:

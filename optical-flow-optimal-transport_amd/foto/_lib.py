@@ -119,7 +119,10 @@ def load(path):
         raise FotoError(f"libfoto.so not found at {path}; build it with "
                         "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C csrc`")
     L = ctypes.CDLL(path)
+    lax = os.environ.get("FOTO_LIB_LAX") == "1"   # A/B runs against older builds (tools/ab_lib.sh)
     for name, (res, args) in SIGNATURES.items():
+        if lax and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
