@@ -1583,6 +1583,22 @@ __device__ long long foto_plan_clock[8];
 #define FOTO_PLAN_STAMP(k)
 #endif
 
+// n / d on the plan's critical chain: v_rcp_f64, one Newton step and one residual correction (5
+// dependent FMAs instead of the ~10-instruction IEEE division sequence; within an ulp of n / d)
+#ifndef FOTO_PLAN_RCP
+#define FOTO_PLAN_RCP 0
+#endif
+__device__ __forceinline__ double plan_div(double n, double d) {
+#if FOTO_PLAN_RCP
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    const double q = n * r;
+    return fma(fma(-d, q, n), r, q);
+#else
+    return n / d;
+#endif
+}
+
 __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* xb /* shared, 3 NG + 2 */, int init,
                                 double rtol, int maxiter) {
     const int lane = threadIdx.x & 63;
@@ -1642,7 +1658,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         }
         if (uni(rho == 0.0 || sqrt(rho) < S.atol)) { conv = true; break; }
         const bool first = (S.k + i == 0);
-        const double beta = first ? 0.0 : rho / rho_prev;
+        const double beta = first ? 0.0 : plan_div(rho, rho_prev);
         const double Pn = first ? R : beta * P + R;
 #if FOTO_PLAN_DPP == 2
         const double Q = plan_mul_lam_dpp(Pn, S.c0, S.c1);
@@ -1655,7 +1671,7 @@ __device__ void sstep_plan_wave(SStep* Sg, SStep S, const double* tot, double* x
         const double den = plan_ip(Pn, Q, hrow, xb, &cr);
 #endif
         if (i > 0 && uni(!(cr <= 1.0))) break;
-        const double alpha = rho / den;
+        const double alpha = plan_div(rho, den);
         R = R - alpha * Q;
         P = Pn;
         rho_prev = rho;
@@ -2396,10 +2412,13 @@ constexpr int TC_NTH = 256;
 #define FOTO_TC_WPE 4
 #endif
 
-template <int NTT>
+// PLAN: single shard, the last block plans the first pass; otherwise (a sharded box) it stores
+// this rank's INIT moments at gath[rank * NACC] for the all-gather and k_spec_s2_plan
+template <int NTT, bool PLAN>
 __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_WPE))) void k_dct_t_fwd_init(SpecTab T, const double* __restrict__ Ch,
                                                            const double* __restrict__ in, double* __restrict__ bh,
-                                                           SStep* Sg, RedBuf rb, double rtol, int maxiter) {
+                                                           SStep* Sg, RedBuf rb, double rtol, int maxiter,
+                                                           double* gath, int rank) {
     constexpr int H = TCol<NTT>::H;
     const int64_t ncols = (int64_t)T.nyl * T.Nx;
     const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
@@ -2454,6 +2473,10 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
     if (!sp_reduce_last_rs<NMOM, TC_NTH>(acc, rb, tot)) return;
     for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
     __syncthreads();
+    if (!PLAN) {
+        for (int m = threadIdx.x; m < NACC; m += TC_NTH) gath[rank * NACC + m] = tot[m];
+        return;
+    }
     if (threadIdx.x >= 64) return;
     __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
     sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
@@ -2495,11 +2518,146 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
     }
 }
 
+// ---------------------------------------------------------------------------- t axis, two waves per column
+// Columns too long for one thread's registers (Nt = 64 at BASELINE config 4, 1024 x 1024 x 64:
+// 32 folded pairs + 32 outputs + the INIT moments would need ~180 VGPRs).  A wave pair shares 64
+// columns: the even wave (role 0) owns the even outputs k = 2m (E s, s_j = x_j + x_{NTT-1-j}), the
+// odd wave (role 1) the odd ones (O d, d_j = x_j - x_{NTT-1-j}).  Each wave reads the whole column
+// itself (the partner's second read of the same lines is an L2 hit), so the forward needs no
+// exchange; the inverse exchanges its half sums e_j / o_j through LDS in chunks of 8 rows
+// (out_j = e_j + o_j, out_{NTT-1-j} = e_j - o_j).  Per wave the matrix half is wave-uniform
+// (E or O: scalar loads), and every plane is read and written as 64 contiguous doubles per
+// wave instruction -- the strided FFT this replaces ran at ~1 TB/s (64 planes 8 MB apart per
+// block).
+constexpr int TP_CH = 8;   // inverse: rows per LDS exchange chunk
+
+// (64 points: 32 folded values + 16 moment sums + the recurrence need ~130 VGPRs: 3 waves per
+// SIMD, no spills)
+template <int NTT, bool PLAN>
+__global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(NTT > 48 ? 3 : 4))) void k_dct_tp_fwd_init(
+        SpecTab T, const double* __restrict__ Ch, const double* __restrict__ in, double* __restrict__ bh, SStep* Sg,
+        RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
+    constexpr int H = NTT / 2;
+    static_assert(NTT % 2 == 0 && H % TP_CH == 0, "even column length, whole exchange chunks");
+    const int64_t ncols = (int64_t)T.nyl * T.Nx;
+    const int lane = threadIdx.x & 63;
+    const int role = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 1);       // 0 even, 1 odd
+    const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    const int64_t c = ((int64_t)blockIdx.x * (TC_NTH / 128) + pair) * 64 + lane;
+    const SStep S0 = *Sg;
+    const double c0 = S0.ic0, ic1 = 1.0 / S0.ic1;   // INIT interval (previous solve's b^ measure)
+    double acc[NMOM];
+#pragma unroll
+    for (int m = 0; m < NMOM; ++m) acc[m] = 0.0;
+    __shared__ double mts[NTT];
+    for (int i = threadIdx.x; i < NTT; i += TC_NTH) mts[i] = T.mt[i];
+    __syncthreads();
+    if (c < ncols) {
+        const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
+        const double myv = T.my[ky], mxv = T.mx[kx];
+        const double sg = role ? -1.0 : 1.0;
+        double v[H];   // s (even wave) or d (odd wave)
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = in[j * ncols + c] + sg * in[(NTT - 1 - j) * ncols + c];
+        const double* M = Ch + role * H * H;   // E or O, wave-uniform
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            double X = 0.0;
+#pragma unroll
+            for (int j = 0; j < H; ++j) X = fma(M[m * H + j], v[j], X);
+            const int k = 2 * m + role;
+            bh[k * ncols + c] = X;
+            const double lam = T.reps + T.r * ((mts[k] + myv) + mxv);   // spec_lam's order
+            const double x = (lam - c0) * ic1, x2 = x + x, rr = X * X;
+            acc[0] += rr;
+            acc[1] = fma(x, rr, acc[1]);
+            double tm2 = 1.0, tm1 = x;
+#pragma unroll
+            for (int mm = 2; mm < NMOM; ++mm) {
+                const double t = fma(x2, tm1, -tm2);
+                acc[mm] = fma(t, rr, acc[mm]);
+                tm2 = tm1;
+                tm1 = t;
+            }
+        }
+    }
+    __shared__ double tot[NACC];
+    if (!sp_reduce_last_rs<NMOM, TC_NTH>(acc, rb, tot)) return;
+    for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
+    __syncthreads();
+    if (!PLAN) {
+        for (int m = threadIdx.x; m < NACC; m += TC_NTH) gath[rank * NACC + m] = tot[m];
+        return;
+    }
+    if (threadIdx.x >= 64) return;
+    __shared__ __attribute__((aligned(16))) double xb[3 * NG + 2];
+    sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
+}
+
+template <int NTT>
+__global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_dct_tp_inv_xhat(
+        SpecTab T, const double* __restrict__ Ch, const double* __restrict__ bh, const double* __restrict__ rh,
+        const SStep* Sg, double* __restrict__ out) {
+    constexpr int H = NTT / 2;
+    const int64_t ncols = (int64_t)T.nyl * T.Nx;
+    const int lane = threadIdx.x & 63;
+    const int role = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 1);
+    const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    const int64_t c = ((int64_t)blockIdx.x * (TC_NTH / 128) + pair) * 64 + lane;
+    const bool ok = c < ncols;
+    if (Sg->k == 0) rh = bh;   // no pass ran: r = b^, x^ = 0
+    __shared__ double xs[TC_NTH / 128][2][TP_CH][64];   // [pair][role][row of chunk][column]
+    double xk[H];   // x^_{2m + role}
+    if (ok) {
+        const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            const int k = 2 * m + role;
+            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+            xk[m] = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < H; ++m) xk[m] = 0.0;
+    }
+    const double* M = Ch + role * H * H;
+#pragma unroll
+    for (int j0 = 0; j0 < H; j0 += TP_CH) {
+#pragma unroll
+        for (int jj = 0; jj < TP_CH; ++jj) {
+            double e = 0.0;
+#pragma unroll
+            for (int m = 0; m < H; ++m) e = fma(M[m * H + j0 + jj], xk[m], e);
+            xs[pair][role][jj][lane] = e;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < TP_CH; ++jj) {
+            const double e = xs[pair][0][jj][lane], o = xs[pair][1][jj][lane];
+            const int j = j0 + jj;
+            if (ok) {
+                if (role == 0) out[j * ncols + c] = e + o;
+                else out[(NTT - 1 - j) * ncols + c] = e - o;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+#define FOTO_TPAIR_SIZES(X) X(48) X(64)
+
 #define FOTO_TCOL_SIZES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(32)
 
 static bool tcol_supported(int n) {
 #define FOTO_TCOL_CASE(NN) if (n == NN) return true;
     FOTO_TCOL_SIZES(FOTO_TCOL_CASE)
+    FOTO_TPAIR_SIZES(FOTO_TCOL_CASE)
+#undef FOTO_TCOL_CASE
+    return false;
+}
+static bool tpair_size(int n) {
+#define FOTO_TCOL_CASE(NN) if (n == NN) return true;
+    FOTO_TPAIR_SIZES(FOTO_TCOL_CASE)
 #undef FOTO_TCOL_CASE
     return false;
 }
@@ -2717,7 +2875,7 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     }
     {
         const char* e = getenv("FOTO_TCOL");   // 0: t axis by dct_pass + separate INIT / xhat passes (A/B runs)
-        P->tcol = world == 1 && sstep == 2 && tcol_supported(g.Nt) && !(e && atoi(e) == 0);
+        P->tcol = sstep == 2 && tcol_supported(g.Nt) && !(e && atoi(e) == 0);
     }
     if (P->tcol) {
         const int H = g.Nt / 2;
@@ -2731,7 +2889,8 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         FOTO_TRY(P->alloc(ch.size() * 8, &b));
         P->Cth = (double*)b;
         FOTO_HIP_CHECK(hipMemcpy(P->Cth, ch.data(), ch.size() * 8, hipMemcpyHostToDevice));
-        P->tcol_nb = (int)(((int64_t)P->nyl * g.Nx + TC_NTH - 1) / TC_NTH);
+        const int per_block = tpair_size(g.Nt) ? TC_NTH / 2 : TC_NTH;   // wave pairs: 64 columns per 2 waves
+        P->tcol_nb = (int)(((int64_t)P->nyl * g.Nx + per_block - 1) / per_block);
     }
     const int cap = std::max({2 * P->nblocks, NACC * P->nblocks2, NMOM * P->tcol_nb});
     FOTO_TRY(P->alloc(sizeof(double) * (cap + 8), &b));
@@ -2882,18 +3041,34 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
     return hipGetLastError();
 }
 
+// plan (forward): single shard, the kernel plans the first pass; sharded, it leaves this rank's INIT
+// moments in gath for the all-gather
 static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* out, double rtol, int maxiter,
-                              hipStream_t s) {
+                              hipStream_t s, bool plan = true) {
     const SpecTab T = P->tab();
     const int nb = P->tcol_nb;
 #define FOTO_TCOL_LAUNCH(NN)                                                                                       \
     if (P->g.Nt == NN) {                                                                                           \
         if (inv) k_dct_t_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);                  \
-        else k_dct_t_fwd_init<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter);        \
+        else if (plan) k_dct_t_fwd_init<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol,  \
+                                                                      maxiter, P->gath, P->rank);                  \
+        else k_dct_t_fwd_init<NN, false><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter,  \
+                                                               P->gath, P->rank);                                  \
         return hipGetLastError();                                                                                  \
     }
     FOTO_TCOL_SIZES(FOTO_TCOL_LAUNCH)
 #undef FOTO_TCOL_LAUNCH
+#define FOTO_TPAIR_LAUNCH(NN)                                                                                      \
+    if (P->g.Nt == NN) {                                                                                           \
+        if (inv) k_dct_tp_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);                 \
+        else if (plan) k_dct_tp_fwd_init<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, \
+                                                                       maxiter, P->gath, P->rank);                 \
+        else k_dct_tp_fwd_init<NN, false><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter, \
+                                                                P->gath, P->rank);                                 \
+        return hipGetLastError();                                                                                  \
+    }
+    FOTO_TPAIR_SIZES(FOTO_TPAIR_LAUNCH)
+#undef FOTO_TPAIR_LAUNCH
     return hipErrorNotSupported;
 }
 
@@ -3068,13 +3243,17 @@ int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, P->nyl * g.Nx, P->tmp, P->bh, s));   // box tmp -> b^
+    if (P->tcol)   // box tmp -> b^ and this rank's INIT moments -> gath (cg_begin then launches nothing)
+        FOTO_HIP_CHECK(launch_tcol(P, false, P->tmp, nullptr, 0.0, 0, s, false));
+    else
+        FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, P->nyl * g.Nx, P->tmp, P->bh, s));   // box tmp -> b^
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
     return 0;
 }
 
 int SpectralPlan::cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
+    if (P->tcol) return 0;   // the column kernel of fwd_t took the INIT moments
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, P->gath, s));
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * P->nbox());
@@ -3115,6 +3294,11 @@ int SpectralPlan::inv_t(KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
+    if (P->tcol) {   // x^ and the inverse t-DCT in one column kernel: tmp = box of x~ (box_out)
+        FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, P->tmp, 0.0, 0, s));
+        if (kt) kt->stop(e, s, FOTO_K_DCT, 3.0 * 8.0 * P->nbox());
+        return 0;
+    }
     FOTO_HIP_CHECK(launch_xhat(P, s));                                              // tmp = x^
     FOTO_HIP_CHECK(dct_pass(P, 2, true, 1, P->nyl * g.Nx, P->tmp, P->rh, s));    // rh = box of x~
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
@@ -3137,7 +3321,10 @@ int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t 
 
 double* SpectralPlan::stage() const { return ((SpecImpl*)impl)->stage; }
 double* SpectralPlan::box_in() const { return ((SpecImpl*)impl)->tmp; }
-double* SpectralPlan::box_out() const { return ((SpecImpl*)impl)->rh; }
+double* SpectralPlan::box_out() const {
+    const SpecImpl* P = (const SpecImpl*)impl;
+    return P->tcol ? P->tmp : P->rh;
+}
 double* SpectralPlan::gath() const { return ((SpecImpl*)impl)->gath; }
 int SpectralPlan::moments() { return NACC; }
 int SpectralPlan::y0() const { return ((SpecImpl*)impl)->y0; }

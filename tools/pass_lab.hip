@@ -270,6 +270,64 @@ int main(int argc, char** argv) {
                (ck[3] - ck[0]) * 0.01, (ck[4] - ck[3]) * 0.01, (ck[5] - ck[4]) * 0.01, (ck[1] - ck[5]) * 0.01);
 #endif
     }
+    // the first pass of a solve: the plan from the INIT moments of r_0 = b (q = 0, k = 0), as in
+    // a real solve a well-conditioned measure -> an 8-step plan (the state above is random r, q
+    // with made-up scalars, which plans 1 step)
+    {
+        SStep Si = S0;
+        Si.k = 0; Si.nsteps = 0; Si.fin = 0; Si.done = 0; Si.pend = 0; Si.rho_prev = 0.0; Si.atol = 1e-30;
+        Si.c0 = Si.gc0 = Si.ic0 = 6.005; Si.c1 = Si.gc1 = Si.ic1 = 5.995;
+        (void)hipMemcpy(Sg2, &Si, sizeof(SStep), hipMemcpyHostToDevice);
+        (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, true, false, 0);   // INIT moments -> gath2
+        if (hipDeviceSynchronize() != hipSuccess) { printf("fault\n"); return 2; }
+        std::vector<double> gsave(NACC);
+        (void)hipMemcpy(gsave.data(), gath2, 8 * NACC, hipMemcpyDeviceToHost);
+        Si.pend = 1;
+        float best = 1e9;
+        for (int rep = 0; rep < 20; ++rep) {
+            (void)hipMemcpy(Sg2, &Si, sizeof(SStep), hipMemcpyHostToDevice);
+            (void)hipMemcpy(gath2, gsave.data(), 8 * NACC, hipMemcpyHostToDevice);
+            (void)hipEventRecord(e0);
+            (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, false, true, 0);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            float t;
+            (void)hipEventElapsedTime(&t, e0, e1);
+            if (t < best) best = t;
+        }
+        SStep hS;
+        (void)hipMemcpy(&hS, Sg2, sizeof(SStep), hipMemcpyDeviceToHost);
+        printf("%-44s %6.1f us (single launch; %d steps, pend %d)\n", "ring D=4 first pass, plan from INIT moments",
+               best * 1e3, hS.nsteps, hS.pend);
+        // a solve's pass sequence: from the INIT state, 16 late-planning passes back to back (each
+        // plans from the moments the previous one left), as the solver enqueues them
+        float bseq = 1e9;
+        int kdone = 0, npass = 0;
+        for (int rep = 0; rep < 5; ++rep) {
+            (void)hipMemcpy(Sg2, &Si, sizeof(SStep), hipMemcpyHostToDevice);
+            (void)hipMemcpy(gath2, gsave.data(), 8 * NACC, hipMemcpyHostToDevice);
+            (void)hipEventRecord(e0);
+            for (int i = 0; i < 16; ++i) (void)launch_s2_ring(T, r2, p2, b, Sg2, rb, 1e-6, 1000, gath2, 0, false, true, 0);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            float t;
+            (void)hipEventElapsedTime(&t, e0, e1);
+            if (t < bseq) bseq = t;
+            (void)hipMemcpy(&hS, Sg2, sizeof(SStep), hipMemcpyDeviceToHost);
+            kdone = hS.k + hS.nsteps;
+            npass = hS.passes;
+        }
+        printf("%-44s %6.1f us per pass (16 back to back; %d plans, %d CG iterations planned)\n",
+               "ring D=4 solve sequence from INIT", bseq * 1e3 / 16, npass, kdone);
+#ifdef FOTO_PLAN_CLOCK
+        long long ck[8];
+        (void)hipMemcpyFromSymbol(ck, HIP_SYMBOL(foto_plan_clock), sizeof ck);
+        printf("   block 0 wave 0: moments load + plan %.2f us, then barrier %.2f us\n", (ck[1] - ck[0]) * 0.01,
+               (ck[2] - ck[1]) * 0.01);
+        printf("   plan: to Gram rows %.2f us, steps %.2f us, interval %.2f us, stores %.2f us\n",
+               (ck[3] - ck[0]) * 0.01, (ck[4] - ck[3]) * 0.01, (ck[5] - ck[4]) * 0.01, (ck[1] - ck[5]) * 0.01);
+#endif
+    }
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     return 0;
 }

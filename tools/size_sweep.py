@@ -10,7 +10,9 @@ sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__fi
 from foto.bb import BBSolver  # noqa: E402
 from foto.synthetic import translating_gaussian  # noqa: E402
 
-sizes = sys.argv[1:] or ["64x64x8", "584x388x32", "640x480x32", "1024x1024x64"]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+kern = "--kernels" in sys.argv   # also a timed pass with HIP events around every launch
+sizes = args or ["64x64x8", "584x388x32", "640x480x32", "1024x1024x64"]
 for sz in sizes:
     Nx, Ny, Nt = (int(v) for v in sz.split("x"))
     rho0, rhoT = translating_gaussian(Nx, Ny)
@@ -24,3 +26,14 @@ for sz in sizes:
         dt = time.perf_counter() - t
         its = s.cg_its[-k:]
         print(f"{sz}: {k / dt:8.2f} outer it/s, {1e3 * dt / k:8.3f} ms/outer, CG its {its}", flush=True)
+        if kern:
+            s.reset_stats()
+            s.set_timing(True)
+            s.iterate(k, 0.0, stop_rules=False)
+            s.sync()
+            s.set_timing(False)
+            for name, v in s.stats()["kernels"].items():
+                n = max(v["n"], 1)
+                us = 1e3 * v["ms"] / n
+                print(f"    {name:8s} {v['n']:5d} launches  {us:9.1f} us avg  {v['bytes'] / n / (us * 1e-6) / 1e9:8.1f} GB/s "
+                      f"(algorithmic)  {v['ms'] / k:7.3f} ms per outer", flush=True)
