@@ -623,16 +623,22 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 #ifndef FOTO_FFT_LPB_POW2
 #define FOTO_FFT_LPB_POW2 1    // power-of-two line counts only (whole 128-B segments on strided axes)
 #endif
-template <int M1, int M2>
+// Strided (y-axis) lines get a slightly larger LDS budget: at N = 1024 a line image is 8448 B,
+// so 64 KB held 4 lines (32-B row segments) and 68 KB holds 8 (64 B; still two blocks per CU)
+#ifndef FOTO_FFT_STRIDED_LDS
+#define FOTO_FFT_STRIDED_LDS 69632
+#endif
+template <int M1, int M2, bool CONTIG = true>
 struct FftGeom {
     static constexpr int M = M1 * M2, N = 2 * M;
     static constexpr int LS = 2 * M1 * (M2 + 1);   // doubles per line in LDS
-    // lines per block: LDS (lines + twiddles) <= 64 KB
+    // lines per block: LDS (lines + twiddles) <= 64 KB (contiguous lines) / FOTO_FFT_STRIDED_LDS
     static constexpr int lpb() {
         const int c[8] = {64, 32, 16, 12, 8, 4, 2, 1};
+        const int budget = CONTIG ? 65536 : FOTO_FFT_STRIDED_LDS;
         for (int i = 0; i < 8; ++i)
             if (c[i] <= FOTO_FFT_LPB_MAX && !(FOTO_FFT_LPB_POW2 && c[i] == 12) &&
-                c[i] * LS * 8 + (FOTO_FFT_TW_LDS ? 16 * M : 0) <= 65536)
+                c[i] * LS * 8 + (FOTO_FFT_TW_LDS ? 16 * M : 0) <= budget)
                 return c[i];
         return 1;
     }
@@ -930,6 +936,15 @@ struct FftLines {   // this block's lines: CONTIG rows o0 + l, or columns (o0, i
     int o0, i0, nl;
 };
 
+// Strided lines (CONTIG = false: the y axis, element stride Nx) read LPB adjacent columns per
+// block, LPB * 8 B of every row: 32 B at N = 1024 (LPB 4), a quarter of a 128-B line.  Blocks are
+// dealt to the 8 XCDs round robin, so the neighbours that read the rest of each line sat on
+// other XCDs and every XCD's L2 fetched the whole line (C4's y transforms ran at 1.6-1.8 TB/s).
+// The swizzle gives each XCD a contiguous range of column groups: the blocks that share a
+// line run on one XCD at about the same time (FOTO_FFT_XCD=0: the plain order, A/B builds).
+#ifndef FOTO_FFT_XCD
+#define FOTO_FFT_XCD 1
+#endif
 template <bool CONTIG, int LPB>
 __device__ __forceinline__ FftLines fft_lines(int outer, int inner) {
     FftLines f;
@@ -938,9 +953,15 @@ __device__ __forceinline__ FftLines fft_lines(int outer, int inner) {
         f.i0 = 0;
         f.nl = min(LPB, outer - f.o0);
     } else {
+        int b = blockIdx.x;
+#if FOTO_FFT_XCD
+        constexpr int NXCD = 8;
+        const int nb = gridDim.x, per = nb / NXCD, rem = nb % NXCD, xcd = b % NXCD;
+        b = xcd * per + min(xcd, rem) + b / NXCD;
+#endif
         const int nib = (inner + LPB - 1) / LPB;
-        f.o0 = blockIdx.x / nib;
-        f.i0 = (blockIdx.x - f.o0 * nib) * LPB;
+        f.o0 = b / nib;
+        f.i0 = (b - f.o0 * nib) * LPB;
         f.nl = min(LPB, inner - f.i0);
     }
     return f;
@@ -958,7 +979,7 @@ struct FftRounds {
 template <int M1, int M2, bool CONTIG>
 __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
-    using G = FftGeom<M1, M2>;
+    using G = FftGeom<M1, M2, CONTIG>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
     __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
@@ -1035,7 +1056,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
 template <int M1, int M2, bool CONTIG>
 __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
-    using G = FftGeom<M1, M2>;
+    using G = FftGeom<M1, M2, CONTIG>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
     __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
@@ -1181,8 +1202,8 @@ static hipError_t dct_fft_axis(int outer, int n, int inner, bool inv, const doub
     if (!g_dct_fft || !tab || n < 64 || !fft_factors(n, &m1, &m2)) return hipErrorNotSupported;
 #define FOTO_FFT_LAUNCH(NN, A, B)                                                                  \
     if (n == NN) {                                                                                 \
-        constexpr int LPB = FftGeom<A, B>::LPB;                                                    \
         const bool contig = (inner == 1);                                                          \
+        const int LPB = contig ? FftGeom<A, B, true>::LPB : FftGeom<A, B, false>::LPB;             \
         const int nb = contig ? (outer + LPB - 1) / LPB : outer * ((inner + LPB - 1) / LPB);       \
         if (contig) {                                                                              \
             if (inv) k_dct_fft_inv<A, B, true><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);     \

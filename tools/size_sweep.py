@@ -32,6 +32,13 @@ for sz in sizes:
             s.iterate(k, 0.0, stop_rules=False)
             s.sync()
             s.set_timing(False)
+            import ctypes
+            from foto import _lib
+            n = Nx * Ny * Nt
+            us = (ctypes.c_double * 2)()
+            if n % 2 == 0 and n * 8 < 2 ** 31 and _lib.lib().foto_stream_probe(n, 10, us) == 0:
+                print(f"    stream probe (r, q of this box): {min(us[0], us[1]):8.1f} us = "
+                      f"{32 * n / (min(us[0], us[1]) * 1e-6) / 1e9:7.1f} GB/s", flush=True)
             for name, v in s.stats()["kernels"].items():
                 n = max(v["n"], 1)
                 us = 1e3 * v["ms"] / n
