@@ -14,6 +14,8 @@
 #include <cstddef>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <utility>
 
 #include "foto_internal.h"
 #include "foto_spectral.h"
@@ -28,6 +30,33 @@ void set_error(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
+}
+
+static std::mutex g_pool_mu;
+static std::vector<std::pair<int, hipStream_t>> g_pool;   // (device, stream) free list
+
+int stream_acquire(hipStream_t* out) {
+    int dev = 0;
+    FOTO_HIP_CHECK(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (g_pool[i].first == dev) {
+                *out = g_pool[i].second;
+                g_pool.erase(g_pool.begin() + i);
+                return 0;
+            }
+    }
+    FOTO_HIP_CHECK(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    return 0;
+}
+
+void stream_release(hipStream_t s) {
+    if (!s) return;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back({dev, s});
 }
 
 #define FOTO_NCCL_CHECK(call)                                                                 \
@@ -131,7 +160,10 @@ struct foto_bb_ctx {
         if (hgath) (void)hipHostFree(hgath);
         for (auto e : ph) if (e) (void)hipEventDestroy(e);
         for (auto e : phr) if (e) (void)hipEventDestroy(e);
-        if (s) (void)hipStreamDestroy(s);
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            stream_release(s);
+        }
     }
 };
 
@@ -203,7 +235,7 @@ static int halo(foto_bb_ctx* c, Pick pick) {
 static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     const int64_t nxy = (int64_t)c->Nx * c->Ny;
     if (c->o.device >= 0) FOTO_HIP_CHECK(hipSetDevice(c->o.device));
-    FOTO_HIP_CHECK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+    FOTO_TRY(stream_acquire(&c->s));
     FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hS, sizeof(CGScal)));
     const int W = c->W;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hgath, sizeof(double) * 4 * W));

@@ -17,10 +17,7 @@ namespace {
 struct Scope {   // one call's stream + device allocations
     hipStream_t s = nullptr;
     std::vector<void*> bufs;
-    int init() {
-        FOTO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        return 0;
-    }
+    int init() { return stream_acquire(&s); }
     int dev(size_t n_doubles, double** out) {
         void* p = nullptr;
         FOTO_HIP_CHECK(hipMalloc(&p, std::max<size_t>(n_doubles, 1) * sizeof(double)));
@@ -44,7 +41,7 @@ struct Scope {   // one call's stream + device allocations
     ~Scope() {
         if (s) (void)hipStreamSynchronize(s);
         for (void* p : bufs) (void)hipFree(p);
-        if (s) (void)hipStreamDestroy(s);
+        stream_release(s);
     }
 };
 

@@ -106,10 +106,7 @@ namespace {
 struct EvScope {
     hipStream_t s = nullptr;
     std::vector<void*> bufs;
-    int init() {
-        FOTO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        return 0;
-    }
+    int init() { return stream_acquire(&s); }
     int up(const double* h, size_t n, double** d) {
         if (!h) { *d = nullptr; return 0; }
         void* p;
@@ -129,7 +126,7 @@ struct EvScope {
     ~EvScope() {
         if (s) (void)hipStreamSynchronize(s);
         for (void* p : bufs) (void)hipFree(p);
-        if (s) (void)hipStreamDestroy(s);
+        stream_release(s);
     }
 };
 

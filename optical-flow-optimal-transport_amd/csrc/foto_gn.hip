@@ -9,11 +9,14 @@
 // smoothing with the per-pixel 3x3 block D + v v^T, v = (fx, fy, -f2); FOTO_GN_MG=0 keeps
 // plain block-Jacobi PCG), driven on the device with the same last-block reductions as
 // the BB CG and replayed as a hipGraph.
+#include <chrono>
+
 #include "foto_internal.h"
 
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 namespace foto {
@@ -597,6 +600,12 @@ __global__ __launch_bounds__(NT) void k_gnp_upd(int w, int h, const double* __re
     if (blockIdx.x == 0 && threadIdx.x == 0) S->pad[0] = S->pad[0] + 1;
 }
 
+// device -> mapped pinned host memory, 8 B per lane (writes cross PCIe as the kernel runs)
+__global__ __launch_bounds__(NT) void k_gn_download(int64_t n, const double* __restrict__ x, double* host) {
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i < n) host[i] = x[i];
+}
+
 // ----------------------------------------------------------------------------- V-cycle kernels
 
 __global__ __launch_bounds__(NT) void k_mg_b0(int64_t n, const double* __restrict__ fx, const double* __restrict__ fy,
@@ -866,6 +875,7 @@ struct foto_gn_plan {
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
     CGScal* hS = nullptr;
+    double* hbuf_dev = nullptr;   // hbuf as the device sees it (kernels write u, v, m there)
     double* hbuf = nullptr;   // pinned staging: f1, f2, u, v, m (pageable copies of ~2.5 MB were
                               // pinned on the fly by the runtime: 15-25 ms per solve at 640x480)
     struct Lev {
@@ -892,7 +902,7 @@ struct foto_gn_plan {
         if (base) (void)hipFree(base);
         if (hS) (void)hipHostFree(hS);
         if (hbuf) (void)hipHostFree(hbuf);
-        if (s) (void)hipStreamDestroy(s);
+        stream_release(s);
     }
 };
 
@@ -955,14 +965,30 @@ static int gn_iteration(foto_gn_plan* P, int par) {
     return gn_vcycle(P, P->r, P->z, P->rz_part[par ^ 1]);
 }
 
+// FOTO_GN_TRACE=1: wall time of each plan-creation phase on stderr (first-call cost studies)
+struct GnTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    GnTrace() : on(getenv("FOTO_GN_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[gn plan] %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+
 static int gn_plan_init(foto_gn_plan* P) {
     const int w = P->w, h = P->h;
     const size_t n = (size_t)w * h;
+    GnTrace tr;
     FOTO_HIP_CHECK(hipGetDevice(&P->device));
-    FOTO_HIP_CHECK(hipStreamCreateWithFlags(&P->s, hipStreamNonBlocking));
+    FOTO_TRY(stream_acquire(&P->s));   // (pooled: a new stream cost ~10 ms)
+    tr.mark("stream");
     for (auto& e : P->ev) FOTO_HIP_CHECK(hipEventCreate(&e));
+    tr.mark("events");
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
-    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hbuf, 5 * n * sizeof(double)));
+    tr.mark("pinned scalars");   // (the pinned staging is made during the first solve: gn_staging)
     P->nb_pix = flat_blocks((int64_t)n);
     // level geometry
     int lw = w, lh = h;
@@ -983,6 +1009,7 @@ static int gn_plan_init(foto_gn_plan* P) {
     const size_t nscal = sizeof(CGScal) / sizeof(double) + 1;
     const size_t total = 23 * n + lev_total + 2 * (size_t)P->nb_pix + 2 * (size_t)P->nb_rz + nscal + 64;
     FOTO_HIP_CHECK(hipMalloc((void**)&P->base, total * sizeof(double)));
+    tr.mark("device buffers");
     double* q = P->base;
     P->d1 = q; q += n; P->d2 = q; q += n; P->fx = q; q += n; P->fy = q; q += n; P->ft = q; q += n;
     P->b = q; q += 3 * n; P->x = q; q += 3 * n; P->r = q; q += 3 * n; P->z = q; q += 3 * n;
@@ -1003,7 +1030,21 @@ static int gn_plan_init(foto_gn_plan* P) {
     const hipError_t ec = hipStreamEndCapture(P->s, &P->graph);
     FOTO_TRY(c2);
     FOTO_HIP_CHECK(ec);
+    tr.mark("graph capture");
     FOTO_HIP_CHECK(hipGraphInstantiate(&P->gexec, P->graph, nullptr, nullptr, 0));
+    tr.mark("graph instantiate");
+    return 0;
+}
+
+// The pinned staging (f1, f2 up; u, v, m down), made while the first solve's iterations run:
+// pinning 12 MB took ~3 ms at 640x480, a third of a first call (FOTO_GN_TRACE); that solve
+// uploads from the caller's pageable arrays instead.
+static int gn_staging(foto_gn_plan* P) {
+    if (P->hbuf) return 0;
+    const size_t n = (size_t)P->w * P->h;
+    FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hbuf, 5 * n * sizeof(double)));
+    memset(P->hbuf, 0, 5 * n * sizeof(double));   // first touch on the host, not by the device
+    FOTO_HIP_CHECK(hipHostGetDevicePointer((void**)&P->hbuf_dev, P->hbuf, 0));
     return 0;
 }
 
@@ -1012,12 +1053,18 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     const int w = P->w, h = P->h;
     const int64_t n = (int64_t)w * h;
     hipStream_t s = P->s;
+    GnTrace tr;
     FOTO_HIP_CHECK(hipEventRecord(P->ev[0], s));
-    double* hb = P->hbuf;
-    memcpy(hb, f1, n * sizeof(double));
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, hb, n * sizeof(double), hipMemcpyHostToDevice, s));
-    memcpy(hb + n, f2, n * sizeof(double));
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, hb + n, n * sizeof(double), hipMemcpyHostToDevice, s));
+    if (P->hbuf) {
+        double* hb = P->hbuf;
+        memcpy(hb, f1, n * sizeof(double));
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, hb, n * sizeof(double), hipMemcpyHostToDevice, s));
+        memcpy(hb + n, f2, n * sizeof(double));
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, hb + n, n * sizeof(double), hipMemcpyHostToDevice, s));
+    } else {   // first solve of the plan (gn_staging)
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, f1, n * sizeof(double), hipMemcpyHostToDevice, s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, f2, n * sizeof(double), hipMemcpyHostToDevice, s));
+    }
     FOTO_HIP_CHECK(hipMemsetAsync(P->dS, 0, sizeof(CGScal), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->x, 0, 3 * n * sizeof(double), s));
     FOTO_HIP_CHECK(launch_gn_coeffs(w, h, P->d1, P->d2, P->fx, P->fy, P->ft, s));
@@ -1040,6 +1087,7 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     FOTO_HIP_CHECK(hipGetLastError());
     FOTO_TRY(gn_vcycle(P, P->r, P->z, P->rz_part[0]));
     FOTO_HIP_CHECK(hipEventRecord(P->ev[1], s));
+    tr.mark("solve: setup enqueued");
     // replay pairs of iterations; the first wait comes after the previous solve's count
     int k = 0;
     bool done = false;
@@ -1054,12 +1102,20 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
             ++k;
         }
         FOTO_HIP_CHECK(hipMemcpyAsync(P->hS, P->dS, sizeof(CGScal), hipMemcpyDeviceToHost, s));
+        if (k == chunk) FOTO_TRY(gn_staging(P));   // while the first iterations run
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
         if (P->hS->done) { done = true; break; }
     }
     FOTO_HIP_CHECK(hipEventRecord(P->ev[2], s));
-    FOTO_HIP_CHECK(hipMemcpyAsync(hb + 2 * n, P->x, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    tr.mark("solve: PCG done");
+    // the solution straight into the mapped pinned staging by a kernel: the first large
+    // device-to-host hipMemcpy of a process took 8.5-14.8 ms at 640x480 (0.15-0.4 ms later)
+    FOTO_TRY(gn_staging(P));   // (maxiter 0: no iteration ran)
+    k_gn_download<<<flat_blocks(3 * n), NT, 0, s>>>(3 * n, P->x, P->hbuf_dev + 2 * n);
+    FOTO_HIP_CHECK(hipGetLastError());
     FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    tr.mark("solve: download");
+    const double* hb = P->hbuf;
     memcpy(u, hb + 2 * n, n * sizeof(double));
     memcpy(v, hb + 3 * n, n * sizeof(double));
     memcpy(m, hb + 4 * n, n * sizeof(double));

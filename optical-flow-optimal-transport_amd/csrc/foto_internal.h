@@ -31,6 +31,14 @@ void set_error(const char* fmt, ...);
         if (rc_ < 0) return rc_; \
     } while (0)
 
+// ----------------------------------------------------------------------------- streams
+// Streams come from a process-wide pool (foto_bb.cpp): a hipStreamCreate costs ~10 ms on the
+// MI355X box (FOTO_GN_TRACE), which every BB context, GN plan and per-call scope paid -- a
+// batch of solves paid it per solve.  acquire returns a stream of the current device; release
+// takes back a stream with no work pending (callers synchronise first).  Never destroyed.
+int stream_acquire(hipStream_t* out);
+void stream_release(hipStream_t s);
+
 // ----------------------------------------------------------------------------- geometry
 // One time-slab shard of the (Nt, Ny, Nx) grid: local planes l in [0, nloc) are global
 // planes t0 + l.  Every field array is allocated with one halo plane below (l = -1) and
