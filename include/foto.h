@@ -126,6 +126,11 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double convergence_tol, int u
 /* Flow (u, v, m) from the last phi: utils.opticalflow_from_benamoubrenier.
  * With world > 1 the result lands on rank 0; other ranks may pass NULL.           */
 int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m);
+/* A new pair (rho0, rhoT) of the same size on an existing context: every field, counter and
+ * prediction back to what foto_bb_create leaves, so the solve is bit-identical to one on a
+ * fresh context -- without its allocations, DCT plans and stream (a batch of same-size
+ * frames: run.sh:81-157 runs one solve per sequence).                                     */
+int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT);
 /* Copy this shard's slab range of phi / mu / q to host (t0, nloc via foto_bb_shard). */
 int foto_bb_get_phi(foto_bb_ctx* c, double* phi);
 int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3);

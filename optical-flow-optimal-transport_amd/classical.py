@@ -9,9 +9,7 @@ first access, for callers that inspect the system.
 import sys
 
 import numpy as np
-from scipy import sparse
 
-import operators
 from foto import gn as _gn
 
 
@@ -46,6 +44,9 @@ class GLLOpticalFlow(object):
 
     # host-side view of the assembled system (classical.py:88-111)
     def _assemble_host(self):
+        # scipy only here: importing it costs ~0.3 s per process, a tenth of a batch worker's run
+        from scipy import sparse
+        import operators
         w, h = self.w, self.h
         f1, f2 = self.f1, self.f2
         F2 = f2.reshape(h, w)

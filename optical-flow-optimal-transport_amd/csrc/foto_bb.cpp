@@ -762,6 +762,41 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
     return stopped;
 }
 
+int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
+    if (!c || !rho0 || !rhoT) { set_error("null argument"); return FOTO_ERR_ARG; }
+    if (c->enq_dsp) { set_error("foto_bb_reset: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
+    const int64_t nxy = (int64_t)c->Nx * c->Ny;
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const size_t bytes = (size_t)(s.g.nloc + 2) * (size_t)nxy * sizeof(double);
+        double* fields[] = {s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], s.nu[0], s.nu[1], s.nu[2],
+                            s.phi, s.rv, s.p[0], s.p[1]};
+        for (double* f : fields)   // as ctx_init leaves them: zero, halo planes included
+            if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - nxy, 0, bytes, c->s));
+        FOTO_HIP_CHECK(hipMemsetAsync(s.gath, 0, sizeof(double) * 4 * c->W, c->s));
+        FOTO_HIP_CHECK(hipMemsetAsync(s.rb.ticket, 0, sizeof(unsigned) * 64, c->s));
+        FOTO_HIP_CHECK(hipMemsetAsync(s.S, 0, sizeof(CGScal), c->s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(s.rho0, rho0, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
+        FOTO_HIP_CHECK(hipMemcpyAsync(s.rhoT, rhoT, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
+        FOTO_HIP_CHECK(launch_init_mu(s.g, s.rho0, s.rhoT, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->s));
+        if (s.spec) FOTO_TRY(s.spec->reset(c->s));
+    }
+    c->last_cg = 0;
+    c->last_passes = 0;
+    c->enq_its = c->enq_info = 0;
+    c->have_phi = 0;
+    c->f_ready = false;
+    for (int f = 0; f < 3; ++f) c->fz_src[f] = c->fz_dst[f] = nullptr;
+    c->prev_crit = -1;
+    c->st = foto_bb_stats{};
+    c->kt.resolve();
+    c->kt.reset();
+    c->hpar = c->tail_par = 0;
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
 int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m) {
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
     return flow(c, u, v, m);

@@ -38,6 +38,10 @@ struct SpectralPlan {
     int y0() const;
     int nyl() const;
 
+    // back to the state init() leaves (no solve in flight, no pass-count prediction, the
+    // whole-spectrum interval): a reused context solves a new pair exactly as a fresh one would
+    int reset(hipStream_t s);
+
     ~SpectralPlan();
     void* impl = nullptr;
 };

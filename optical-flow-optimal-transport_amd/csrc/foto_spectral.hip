@@ -2779,6 +2779,13 @@ struct SpecImpl {
 };
 
 // orthonormal DCT-II matrix C[k][j] = s_k cos(pi k (2j+1) / (2n)) (long double on the host)
+// eigenvalues 2 - 2 cos(pi k / n) of the Neumann second difference (the same values dct_matrix gives)
+static void dct_eigen(int n, std::vector<double>& mu) {
+    mu.assign(n, 0.0);
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int k = 0; k < n; ++k) mu[k] = (double)(2.0L - 2.0L * cosl(pi * k / n));
+}
+
 static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, std::vector<double>& mu) {
     C.assign((size_t)n * n, 0.0);
     CT.assign((size_t)n * n, 0.0);
@@ -2840,14 +2847,25 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         FOTO_TRY(P->alloc(NS * 8, &b)); P->stage = (double*)b;
     }
     std::vector<double> C, CT, mu;
+    if (g_dct_fft < 0) {
+        const char* e = getenv("FOTO_DCT_FFT");
+        g_dct_fft = e ? atoi(e) : 1;
+    }
+    // the n x n matrices only for an axis the FFT kernels do not take (dct_fft_axis's rule):
+    // 2 x 3.3 MB of host cosines and blocking copies per 640-axis saved at context creation
     auto up = [&](int n, double** Cd, double** CTd, double** mud) -> int {
-        dct_matrix(n, C, CT, mu);
+        int m1, m2;
+        const bool fft = g_dct_fft && n >= 64 && fft_factors(n, &m1, &m2);
+        if (fft) dct_eigen(n, mu);
+        else dct_matrix(n, C, CT, mu);
         void* p;
-        FOTO_TRY(P->alloc(C.size() * 8, &p)); *Cd = (double*)p;
-        FOTO_TRY(P->alloc(CT.size() * 8, &p)); *CTd = (double*)p;
+        if (!fft) {
+            FOTO_TRY(P->alloc(C.size() * 8, &p)); *Cd = (double*)p;
+            FOTO_TRY(P->alloc(CT.size() * 8, &p)); *CTd = (double*)p;
+            FOTO_HIP_CHECK(hipMemcpy(*Cd, C.data(), C.size() * 8, hipMemcpyHostToDevice));
+            FOTO_HIP_CHECK(hipMemcpy(*CTd, CT.data(), CT.size() * 8, hipMemcpyHostToDevice));
+        }
         FOTO_TRY(P->alloc(mu.size() * 8, &p)); *mud = (double*)p;
-        FOTO_HIP_CHECK(hipMemcpy(*Cd, C.data(), C.size() * 8, hipMemcpyHostToDevice));
-        FOTO_HIP_CHECK(hipMemcpy(*CTd, CT.data(), CT.size() * 8, hipMemcpyHostToDevice));
         FOTO_HIP_CHECK(hipMemcpy(*mud, mu.data(), mu.size() * 8, hipMemcpyHostToDevice));
         return (int)0;
     };
@@ -3338,6 +3356,16 @@ int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t 
     FOTO_HIP_CHECK(dct_pass(P, 0, true, g.nloc * g.Ny, 1, P->tmpp, x, s));       // x
     if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
     return 0;
+}
+
+int SpectralPlan::reset(hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    P->pending = false;
+    P->pend_launched = 0;
+    P->last_passes = 0;
+    FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
+    FOTO_HIP_CHECK(hipMemsetAsync(P->rb.ticket, 0, 8 * sizeof(double), s));
+    return reset_s2(P, s);
 }
 
 double* SpectralPlan::stage() const { return ((SpecImpl*)impl)->stage; }

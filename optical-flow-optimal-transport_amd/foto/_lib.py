@@ -83,6 +83,7 @@ SIGNATURES = {
     "foto_bb_create": (_I, [_D, _D, _I, _I, _I, _Dbl, _Dbl, ctypes.POINTER(BBOpts), ctypes.POINTER(_P)]),
     "foto_bb_iterate": (_I, [_P, _I, _Dbl, _I, ITER_CB, _P, ctypes.POINTER(_I)]),
     "foto_bb_flow": (_I, [_P, _D, _D, _D]),
+    "foto_bb_reset": (_I, [_P, _D, _D]),
     "foto_bb_get_phi": (_I, [_P, _D]),
     "foto_bb_get_state": (_I, [_P, _D, _D]),
     "foto_bb_shard": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),

@@ -5,7 +5,10 @@
 iteration (Python ``str`` of a float64), the CG non-convergence warning of
 benamou_brenier.py:86-87, and (u, v, m) from the trajectory flow extraction.
 """
+import collections
 import ctypes
+import os
+import sys
 
 import numpy as np
 
@@ -68,6 +71,18 @@ class BBSolver:
     def _check(self, rc):
         return check(rc, self._L)
 
+    def reset(self, rho0, rhoT):
+        """Start over on a new pair of the same size: the context's fields, CG state and
+        predictions go back to what construction leaves (foto_bb_reset), so the solve is
+        bit-identical to one on a fresh BBSolver, without its allocations and plans."""
+        nxy = self.Nx * self.Ny
+        self._rho0 = f64(rho0, nxy, "rho0")
+        self._rhoT = f64(rhoT, nxy, "rhoT")
+        self._check(self._L.foto_bb_reset(self._ctx, dptr(self._rho0), dptr(self._rhoT)))
+        self.crit = []
+        self.cg_its = []
+        self.cg_info = []
+
     # -------------------------------------------------------------- lifecycle
     def close(self):
         if getattr(self, "_ctx", None) and self._ctx.value:
@@ -75,6 +90,8 @@ class BBSolver:
             self._ctx = ctypes.c_void_p()
 
     def __del__(self):
+        if sys.is_finalizing():   # libfoto / HIP may already be torn down
+            return
         try:
             self.close()
         except Exception:
@@ -162,6 +179,44 @@ class BBSolver:
         self._check(self._L.foto_bb_sync(self._ctx))
 
 
+# One context per (size, parameters) for a batch of same-size frames (run.sh:81-157 solves one
+# pair per sequence): a context costs its HBM fields, DCT plans and a stream to build, and
+# foto_bb_reset makes a reused one give the same bits as a fresh one.  FOTO_BB_CACHE=0 turns
+# it off; sharded contexts (RCCL rank/world) and explicit libraries are never cached.
+CONTEXT_CACHE_SIZE = 2
+_ctx_cache = collections.OrderedDict()
+
+
+def _cache_enabled(opts):
+    if os.environ.get("FOTO_BB_CACHE", "1") == "0" or CONTEXT_CACHE_SIZE <= 0:
+        return False
+    return (opts.get("library") is None and opts.get("nccl_id") is None
+            and int(opts.get("world", 1)) == 1)
+
+
+def cached_solver(rho0, rhoT, Nt, Nx, Ny, r, reg_epsilon, **opts):
+    """A BBSolver for this size and these options, reset to (rho0, rhoT): reused from the
+    cache when one exists, else created (the least recently used context beyond
+    CONTEXT_CACHE_SIZE is destroyed)."""
+    # FOTO_* tuning variables are read when a context is built: part of its identity
+    env = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("FOTO_")))
+    key = (int(Nt), int(Nx), int(Ny), float(r), float(reg_epsilon), tuple(sorted(opts.items())), env)
+    s = _ctx_cache.pop(key, None)
+    if s is not None:
+        s.reset(rho0, rhoT)
+    else:
+        s = BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=reg_epsilon, **opts)
+    _ctx_cache[key] = s
+    while len(_ctx_cache) > CONTEXT_CACHE_SIZE:
+        _ctx_cache.popitem(last=False)[1].close()
+    return s
+
+
+def clear_context_cache():
+    while _ctx_cache:
+        _ctx_cache.popitem()[1].close()
+
+
 def solve(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, max_it=100, *, log=print,
           stats=None, **opts):
     """benamou_brenier.solve on the GPU.  Returns (u, v, m)."""
@@ -174,10 +229,24 @@ def solve(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, ma
             log(f"WARNING: CG did not converge in {info} iterations.")
         log(str(np.float64(crit)) + " (" + str(it + 1) + "/" + str(max_it) + ")")
 
+    if _cache_enabled(opts):
+        s = cached_solver(rho0, rhoT, Nt, Nx, Ny, r, reg_epsilon, **opts)
+        try:
+            return _run(s, max_it, convergence_tol, cb, stats)
+        except BaseException:   # a failed solve leaves no half-used context behind
+            for k, v in list(_ctx_cache.items()):
+                if v is s:
+                    del _ctx_cache[k]
+            s.close()
+            raise
     with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=reg_epsilon, **opts) as s:
-        s.iterate(max_it, convergence_tol=convergence_tol, stop_rules=True, callback=cb)
-        out = s.flow()
-        if stats is not None:
-            stats.update(crit=np.array(s.crit), cg_its=np.array(s.cg_its), cg_info=np.array(s.cg_info),
-                         phi=s.phi(), **s.stats())
+        return _run(s, max_it, convergence_tol, cb, stats)
+
+
+def _run(s, max_it, convergence_tol, cb, stats):
+    s.iterate(max_it, convergence_tol=convergence_tol, stop_rules=True, callback=cb)
+    out = s.flow()
+    if stats is not None:
+        stats.update(crit=np.array(s.crit), cg_its=np.array(s.cg_its), cg_info=np.array(s.cg_info),
+                     phi=s.phi(), **s.stats())
     return out

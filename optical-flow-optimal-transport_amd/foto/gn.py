@@ -1,5 +1,6 @@
 """Gennert-Negahdaripour baseline on the GPU (classical.py:25-130 semantics)."""
 import collections
+import os
 import ctypes
 import sys
 
@@ -98,12 +99,13 @@ def cached_plan(w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
     of one size -- run.sh's per-sequence GN runs -- makes its buffers, multigrid hierarchy and
     graph once, and instances that come and go do not each hold device memory."""
     key = (int(w), int(h), float(alpha), float(lam), float(rtol), int(maxiter))
-    p = _plans.pop(key, None)
+    env = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("FOTO_GN")))   # read at plan build
+    p = _plans.pop(key + (env,), None)
     if p is None:
         p = Plan(*key)
         while len(_plans) >= PLAN_CACHE_SIZE:
             _plans.popitem(last=False)[1].close()
-    _plans[key] = p
+    _plans[key + (env,)] = p
     return p
 
 

@@ -45,8 +45,22 @@ def build_parser():
     return p
 
 
-def main(argv=None):
+def _save_gray(img, w, h, path):
+    Image.fromarray(img.reshape([h, w]), "L").save(path)
+
+
+def main(argv=None, writer=None):
+    """``writer``: an executor (run.py passes a one-thread pool) that takes the output-file
+    writes (.flo, PNGs) off this thread, so the encoding overlaps the next solve; the files
+    are the same.  None: written here, before main returns, as the reference does."""
     args = build_parser().parse_args(argv)
+
+    def emit(fn, *a):
+        if writer is None:
+            fn(*a)
+        else:
+            writer.submit(fn, *a)
+
     np.random.seed(0)
     f1, w, h = utils.openGrayscaleImage(args.f0)
     f2, w, h = utils.openGrayscaleImage(args.f1)
@@ -118,15 +132,15 @@ def main(argv=None):
 
     if args.out:
         print("saving flo file...")
-        utils.saveFlo(w, h, u, v, args.out)
+        emit(utils.saveFlo, w, h, u, v, args.out)
 
     if args.save_reconstruction:
         print("saving reconstruction...")
-        Image.fromarray(np.uint8(255 * rec.reshape([h, w])), "L").save(args.save_reconstruction)
+        emit(_save_gray, np.uint8(255 * rec), w, h, args.save_reconstruction)
 
     if args.save_lum:
         print("saving luminosity...")
-        Image.fromarray(np.uint8(255 * np.clip((m + 1) / 2, 0, 1).reshape([h, w])), "L").save(args.save_lum)
+        emit(_save_gray, np.uint8(255 * np.clip((m + 1) / 2, 0, 1)), w, h, args.save_lum)
 
     print("***********************************")
     return u, v, m

@@ -40,6 +40,8 @@ import subprocess
 import sys
 import zipfile
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(HERE, "bin"))
@@ -188,11 +190,11 @@ def shard(items, rank, world):
     return items[rank::world]
 
 
-def run_main(argv, log_path):
-    """main.py in-process, its stdout captured to log_path."""
+def run_main(argv, log_path, writer=None):
+    """main.py in-process, its stdout captured to log_path; returns (u, v, m)."""
     import main as cli
     with open(log_path, "w") as log, contextlib.redirect_stdout(log):
-        cli.main(argv)
+        return cli.main(argv, writer=writer)
 
 
 def color_flow(flo, png):
@@ -203,16 +205,59 @@ def color_flow(flo, png):
     Image.fromarray(flow_to_color(u, v, w, h), "RGB").save(png)
 
 
-def run_sequence(ds, seq, results, device=-1, extra=()):
+def color_flow_arrays(u, v, w, h, png):
+    """color_flow without the .flo round trip: the same float32 values openFlo returns."""
+    from PIL import Image
+    from color_flow import flow_to_color
+    Image.fromarray(flow_to_color(np.asarray(u, np.float32), np.asarray(v, np.float32), w, h), "RGB").save(png)
+
+
+def touch(path):
+    open(path, "w").close()
+
+
+class Writer:
+    """Output files on one background thread, in submission order (a marker is written after
+    the files of its solve); ``drain`` waits and re-raises the first failure."""
+
+    def __init__(self, threads=1):
+        from concurrent.futures import ThreadPoolExecutor
+        self.pool = ThreadPoolExecutor(max_workers=threads) if threads > 0 else None
+        self.futs = []
+
+    def submit(self, fn, *a):
+        if self.pool is None:
+            fn(*a)
+        else:
+            self.futs.append(self.pool.submit(fn, *a))
+
+    def drain(self):
+        futs, self.futs = self.futs, []
+        for f in futs:
+            f.result()
+
+    def close(self):
+        try:
+            self.drain()
+        finally:
+            if self.pool is not None:
+                self.pool.shutdown()
+
+
+def run_sequence(ds, seq, results, device=-1, extra=(), writer=None):
     """One sequence: diff, then GN and FOTO unless their markers exist (run.sh:86-118)."""
-    from _common import open_gray, save_gray
+    from _common import save_gray
     from data_diff import frame_diff
+    from utils import openGrayscaleImage as open_gray   # decodes shared with main.py's opens
+    own = writer is None
+    if own:
+        writer = Writer(threads=0)
     out = os.path.join(results, ds.name, seq)
     os.makedirs(out, exist_ok=True)
     f0, f1 = ds.frame(seq, 0), ds.frame(seq, 1)
     a, w, h = open_gray(f0)
     b, w, h = open_gray(f1)
-    save_gray(frame_diff(a, b), w, h, os.path.join(out, "diff.png"))
+    writer.submit(save_gray, frame_diff(a, b), w, h, os.path.join(out, "diff.png"))
     done = []
     gt = ds.gt_flow(seq)
     for algo, algo_args in ALGOS:
@@ -225,10 +270,12 @@ def run_sequence(ds, seq, results, device=-1, extra=()):
                 f"--device={device}", *extra]
         if gt:
             argv.append(f"--ground-truth={gt}")
-        run_main(argv, p("log"))
-        color_flow(p("flo"), p("png"))
-        open(marker, "w").close()
+        u, v, _ = run_main(argv, p("log"), writer)
+        writer.submit(color_flow_arrays, u, v, w, h, p("png"))
+        writer.submit(touch, marker)
         done.append(algo)
+    if own:
+        writer.close()
     return done
 
 
@@ -254,11 +301,24 @@ def summarize(args):
 
 
 def worker(args, rank, world, device):
+    """This worker's sequences in order; the output files of one solve are encoded on a
+    background thread while the next one runs (the solver contexts and GN plans are reused
+    across same-size sequences by foto.bb / foto.gn's caches)."""
+    import time
+    t0, t0_wall = time.perf_counter(), time.time()
     mine = shard(jobs(args), rank, world)
-    for ds, seq in mine:
-        done = run_sequence(ds, seq, args.results, device, args.extra)
-        print(f"[rank {rank}/{world}] {ds.name}/{seq}: " + (", ".join(done) if done else "skipped (markers present)"),
-              flush=True)
+    writer = Writer(threads=1)
+    try:
+        for ds, seq in mine:
+            done = run_sequence(ds, seq, args.results, device, args.extra, writer)
+            print(f"[rank {rank}/{world}] {ds.name}/{seq}: " + (", ".join(done) if done else "skipped (markers present)"),
+                  flush=True)
+    finally:
+        writer.close()
+    # the loop's wall clock (batch_bench.py sets it beside the solve times of the benchmark txts)
+    with open(os.path.join(args.results, f".worker{rank}.json"), "w") as f:
+        json.dump({"rank": rank, "world": world, "sequences": len(mine), "loop_s": time.perf_counter() - t0,
+                   "t0_wall": t0_wall, "t1_wall": time.time()}, f)
     return 0
 
 

@@ -9,6 +9,7 @@ Host utilities (image and .flo IO):
   openGrayscaleImage, reconstructTrajectory (single start point), openFlo, saveFlo --
   same semantics and quirks as utils.py:25-292.
 """
+import os
 import math  # noqa: F401  (kept for API parity with the reference module)
 
 import numpy as np
@@ -18,11 +19,28 @@ from foto import evaluate as _ev
 from foto import ops as _ops
 
 
+_frames = {}   # (path, mtime_ns, size) -> (f, w, h): the last few decoded frames
+
+
 def openGrayscaleImage(inputPathname):
-    """8-bit grayscale -> flat float64 in [0, 1], width, height (utils.py:25-42)."""
-    f = np.asarray(Image.open(inputPathname).convert("L"))
-    h, w = f.shape
-    return f.reshape(-1) / 255, w, h
+    """8-bit grayscale -> flat float64 in [0, 1], width, height (utils.py:25-42).  A batch
+    worker opens each frame three times (diff, GN, FOTO); the last 4 decodes are kept, keyed
+    by path, modification time and size, and handed out as copies."""
+    try:
+        st = os.stat(inputPathname)
+        key = (os.path.abspath(inputPathname), st.st_mtime_ns, st.st_size)
+    except (OSError, TypeError):   # file objects and the like: no caching
+        key = None
+    hit = _frames.get(key) if key else None
+    if hit is None:
+        f = np.asarray(Image.open(inputPathname).convert("L"))
+        h, w = f.shape
+        hit = (f.reshape(-1) / 255, w, h)
+        if key:
+            _frames[key] = hit
+            while len(_frames) > 4:
+                del _frames[next(iter(_frames))]
+    return hit[0].copy(), hit[1], hit[2]
 
 
 def reconstructTrajectory(xStart, yStart, u, v, Nx, Ny, Nt):

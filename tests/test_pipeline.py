@@ -69,7 +69,7 @@ def test_prepare(tmp_path):
 
 def _stub_solver(monkeypatch, calls):
     """main.py stand-in: records argv, writes the files main.py would."""
-    def fake(argv, log_path):
+    def fake(argv, log_path, writer=None):
         calls.append(argv)
         kv = dict(a[2:].split("=", 1) for a in argv if a.startswith("--") and "=" in a)
         f, w, h = open_gray(argv[0])
@@ -80,7 +80,35 @@ def _stub_solver(monkeypatch, calls):
         for k in ("save-reconstruction", "save-lum"):
             Image.fromarray(np.zeros((h, w), np.uint8), "L").save(kv[k])
         open(log_path, "w").close()
+        return u, v, np.zeros(w * h)
     monkeypatch.setattr(pipeline, "run_main", fake)
+
+
+def test_color_from_arrays_matches_flo_round_trip(tmp_path):
+    """The background writer colours (u, v) directly; the PNG is byte-identical to colouring
+    the saved .flo (run.sh:104 reads the .flo)."""
+    rng = np.random.default_rng(3)
+    w, h = 37, 23
+    u, v = rng.normal(0, 2.5, w * h), rng.normal(0, 1.5, w * h)
+    utils.saveFlo(w, h, u, v, str(tmp_path / "a.flo"))
+    pipeline.color_flow(str(tmp_path / "a.flo"), str(tmp_path / "a.png"))
+    pipeline.color_flow_arrays(u, v, w, h, str(tmp_path / "b.png"))
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "a.png")), np.asarray(Image.open(tmp_path / "b.png")))
+
+
+def test_writer_order_and_errors(tmp_path):
+    w = pipeline.Writer(threads=1)
+    seen = []
+    for i in range(20):
+        w.submit(seen.append, i)
+    w.drain()
+    assert seen == list(range(20))
+
+    def boom():
+        raise OSError("disk full")
+    w.submit(boom)
+    with pytest.raises(OSError):
+        w.close()
 
 
 def test_run_loop_markers_and_restart(tmp_path, monkeypatch):

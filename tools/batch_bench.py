@@ -59,25 +59,43 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--seqs", type=int, default=len(SIZES))
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "batch"))
+    ap.add_argument("--json", default=None, help="also write the summary line here")
+    ap.add_argument("--cprofile", default=None, help="run run.py under cProfile, stats to this file")
     args = ap.parse_args()
     shutil.rmtree(args.out, ignore_errors=True)
     frames, gt = build(args.out, args.seqs)
     res = os.path.join(args.out, "results")
-    t = time.perf_counter()
-    rc = subprocess.run([sys.executable, os.path.join(PKG, "run.py"), "run", f"--gpus={args.gpus}",
+    t, t_wall = time.perf_counter(), time.time()
+    prof = ["-m", "cProfile", "-o", args.cprofile] if args.cprofile else []
+    rc = subprocess.run([sys.executable, *prof, os.path.join(PKG, "run.py"), "run", f"--gpus={args.gpus}",
                          f"--data={os.path.join(args.out, 'nodata')}", f"--results={res}",
                          f"--dataset=synthetic={frames}:{gt}"]).returncode
-    wall = time.perf_counter() - t
+    wall, t_end = time.perf_counter() - t, time.time()
     rows = json.load(open(os.path.join(res, "summary.json")))
     print(f"{'sequence':<12} {'algo':<5} {'time s':>7} {'AEE px':>8} {'AAE rad':>8} {'IE':>8}")
     for r in rows:
         print(f"{r['sequence']:<12} {r['algo']:<5} {r['time']:7.3f} {r.get('EE-mean', float('nan')):8.4f} "
               f"{r.get('AE-mean', float('nan')):8.4f} {r['IE']:8.4f}")
+    solve_s = float(sum(r["time"] for r in rows))
+    workers = [json.load(open(os.path.join(res, f))) for f in sorted(os.listdir(res)) if f.startswith(".worker")]
+    loop_s = max((x["loop_s"] for x in workers), default=float("nan"))
+    # solve_s: the solver wall clocks main.py prints (time), summed over every solve of every
+    # worker; loop_s: the slowest worker's whole loop (frame IO, diff / rec / lum / colour PNGs,
+    # errors, markers); wall_s: the run.py process tree, interpreter start and HIP init included
     out = {"sequences": args.seqs, "gpus": args.gpus, "wall_s": round(wall, 2), "rc": rc,
+           "loop_s": round(loop_s, 3), "solve_s": round(solve_s, 3),
+           # process start -> first worker loop, last worker loop end -> process tree exit
+           "startup_s": round(min((x["t0_wall"] for x in workers), default=t_wall) - t_wall, 3),
+           "teardown_s": round(t_end - max((x["t1_wall"] for x in workers), default=t_end), 3),
+           "loop_over_solve": round(loop_s * args.gpus / solve_s, 3) if solve_s else None,
+           "wall_over_solve": round(wall * args.gpus / solve_s, 3) if solve_s else None,
            "sequences_per_s": round(args.seqs / wall, 3),
            "mean_AEE": {a: float(np.mean([r["EE-mean"] for r in rows if r["algo"] == a])) for a in ("gn", "foto")},
            "data": "synthetic translations at Middlebury-2 sizes (no Middlebury offline)"}
     print(json.dumps(out))
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump({**out, "rows": rows}, f)
     return rc
 
 
