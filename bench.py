@@ -345,7 +345,7 @@ def main():
             "data": "synthetic (translating Gaussian pair, SURVEY.md §8(d); no Middlebury offline)",
             "config": {"workload": "FOTO Benamou-Brenier outer iteration, 640x480x32, r=1, eps=1e-2, "
                                    "CG rtol=1e-6 (scipy rule), stop rules off",
-                       "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral-cg", "spectral-sstep8"][args.cg_mode],
+                       "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral-cg", "spectral-sstep8", "spectral-gauss"][args.cg_mode],
                        "parallelism": f"time-slab x{world}" if world > 1 else "single GPU"},
             "cg_iters_per_step": round(float(np.mean(cg_steps)), 2) if cg_steps else None,
             "cg_iters_per_s": round(float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,

@@ -61,7 +61,7 @@ int foto_bb_rhs(const double* mu3, const double* q3, const double* rho0, const d
 /* scipy.sparse.linalg.cg(A, b, rtol, maxiter) with A = -r L_st + r eps I, x0 = 0
  * (benamou_brenier.py:85).  Returns info (0 converged, maxiter otherwise) or < 0;
  * *iterations = CG iterations run.  mode: 0 = stencil CG, 1 = spectral CG,
- * 2 = spectral s-step CG (the foto_bb_opts.cg_mode values).                        */
+ * 2 = spectral s-step CG, 3 = Gauss-compressed spectral CG (foto_bb_opts.cg_mode). */
 int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double eps, double rtol, int maxiter,
             int mode, double* x, int* iterations);
 /* utils.opticalflow_from_benamoubrenier(phi, Nt, Nx, Ny, grad('N'), div('D'))
@@ -80,7 +80,9 @@ typedef struct {
     int cg_mode;          /* 0 = stencil CG (7-point matvec), 1 = spectral CG (DCT-II      */
                           /* eigenbasis, one pass / iteration), 2 = spectral s-step CG     */
                           /* (default; one pass / up to 8 iterations, any world; mode 1    */
-                          /* needs world == 1; eps <= 0 selects mode 0)                    */
+                          /* needs world == 1; eps <= 0 selects mode 0), 3 = spectral CG   */
+                          /* on the Gauss-compressed measure of b^ (one read of b^, the    */
+                          /* recurrence on 2048 nodes; any world)                          */
     int rank, world;      /* time-slab sharding over `world` processes (RCCL); 1 = single  */
     const void* nccl_id;  /* 128-byte ncclUniqueId (foto_nccl_unique_id on rank 0)         */
     int virtual_ranks;    /* >1: shard over this many in-process slabs on ONE device       */

@@ -286,7 +286,7 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rho0, rho0, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
         FOTO_HIP_CHECK(hipMemcpyAsync(s.rhoT, rhoT, nxy * sizeof(double), hipMemcpyHostToDevice, c->s));
         FOTO_HIP_CHECK(launch_init_mu(s.g, s.rho0, s.rhoT, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->s));
-        if (c->o.cg_mode == 1 || c->o.cg_mode == 2) {
+        if (c->o.cg_mode >= 1 && c->o.cg_mode <= 3) {
             s.spec.reset(new SpectralPlan());
             FOTO_TRY(s.spec->init(s.g, s.rank, W, c->r, c->eps, c->o.cg_mode, c->s));
         }
@@ -362,6 +362,28 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_local(sp->rv, kt, c->s));
     FOTO_TRY(alltoall_spec(c, true));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_t(kt, c->s));
+    if (c->sh[0]->spec->gauss()) {
+        // Gauss-compressed CG: one all-gather of the boxes' histograms (summed in rank order on
+        // every rank), the small serial solve on every rank, the inverse from the table
+        for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_measure(kt, c->s));
+        FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gauss_hist(); }, SpectralPlan::gauss_hist_size()));
+        for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_solve(rtol, maxiter, kt, c->s));
+        int ok = 1;
+        for (auto& sp : c->sh) {
+            int k_ok = 0;
+            FOTO_TRY(sp->spec->gauss_wait(maxiter, &k_ok, iters, info, c->s));
+            ok = ok && k_ok;   // identical on every shard and rank (same gathered histograms)
+        }
+        if (ok) {
+            for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
+            for (auto& sp : c->sh) sp->spec->gauss_end();
+            FOTO_TRY(alltoall_spec(c, false));
+            for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
+            c->last_cg = *iters;
+            return 0;
+        }
+        c->st.cg_redo += 1;   // the s-step CG from b^ (cg_begin takes its INIT moments)
+    }
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_begin(rtol, maxiter, kt, c->s));
     FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));

@@ -38,6 +38,17 @@ struct SpectralPlan {
     int y0() const;
     int nyl() const;
 
+    // ---- Gauss-compressed CG (cg_mode 3), sharded phases: fwd_t (plain t-DCT), gauss_measure
+    // (this box's histogram -> gauss_hist() slot rank), all-gather of gauss_hist_size() doubles,
+    // gauss_solve, gauss_wait (host sync; !ok: redo with cg_begin / cg_pass from b^), inv_t, ...
+    bool gauss() const;
+    static int gauss_hist_size();
+    double* gauss_hist() const;
+    int gauss_measure(KTimer* kt, hipStream_t s);
+    int gauss_solve(double rtol, int maxiter, KTimer* kt, hipStream_t s);
+    int gauss_wait(int maxiter, int* ok, int* iters, int* info, hipStream_t s);
+    void gauss_end();
+
     // back to the state init() leaves (no solve in flight, no pass-count prediction, the
     // whole-spectrum interval): a reused context solves a new pair exactly as a fresh one would
     int reset(hipStream_t s);

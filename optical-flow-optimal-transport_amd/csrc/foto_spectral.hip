@@ -2433,9 +2433,11 @@ constexpr int TC_NTH = 256;
 #define FOTO_TC_WPE 4
 #endif
 
-// PLAN: single shard, the last block plans the first pass; otherwise (a sharded box) it stores
-// this rank's INIT moments at gath[rank * NACC] for the all-gather and k_spec_s2_plan
-template <int NTT, bool PLAN>
+// MODE 2 (single shard): the last block plans the first pass; MODE 1 (a sharded box): it stores
+// this rank's INIT moments at gath[rank * NACC] for the all-gather and k_spec_s2_plan; MODE 0:
+// b^ only (the Gauss-compressed CG takes its own measure of b^)
+constexpr int TC_PLAIN = 0, TC_GATH = 1, TC_PLAN = 2;
+template <int NTT, int MODE>
 __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_WPE))) void k_dct_t_fwd_init(SpecTab T, const double* __restrict__ Ch,
                                                            const double* __restrict__ in, double* __restrict__ bh,
                                                            SStep* Sg, RedBuf rb, double rtol, int maxiter,
@@ -2465,6 +2467,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
         }
         auto emit = [&](int k, double X) {
             bh[k * ncols + c] = X;
+            if constexpr (MODE == TC_PLAIN) return;
             const double lam = T.reps + T.r * ((mts[k] + myv) + mxv);   // spec_lam's order
             const double x = (lam - c0) * ic1, x2 = x + x, rr = X * X;
             acc[0] += rr;
@@ -2490,11 +2493,12 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
             emit(2 * m + 1, o);
         }
     }
+    if constexpr (MODE == TC_PLAIN) return;
     __shared__ double tot[NACC];
     if (!sp_reduce_last_rs<NMOM, TC_NTH>(acc, rb, tot)) return;
     for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
     __syncthreads();
-    if (!PLAN) {
+    if (MODE == TC_GATH) {
         for (int m = threadIdx.x; m < NACC; m += TC_NTH) gath[rank * NACC + m] = tot[m];
         return;
     }
@@ -2554,7 +2558,7 @@ constexpr int TP_CH = 8;   // inverse: rows per LDS exchange chunk
 
 // (64 points: 32 folded values + 16 moment sums + the recurrence need ~130 VGPRs: 3 waves per
 // SIMD, no spills)
-template <int NTT, bool PLAN>
+template <int NTT, int MODE>
 __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(NTT > 48 ? 3 : 4))) void k_dct_tp_fwd_init(
         SpecTab T, const double* __restrict__ Ch, const double* __restrict__ in, double* __restrict__ bh, SStep* Sg,
         RedBuf rb, double rtol, int maxiter, double* gath, int rank) {
@@ -2588,6 +2592,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(NTT > 48
             for (int j = 0; j < H; ++j) X = fma(M[m * H + j], v[j], X);
             const int k = 2 * m + role;
             bh[k * ncols + c] = X;
+            if constexpr (MODE == TC_PLAIN) continue;
             const double lam = T.reps + T.r * ((mts[k] + myv) + mxv);   // spec_lam's order
             const double x = (lam - c0) * ic1, x2 = x + x, rr = X * X;
             acc[0] += rr;
@@ -2602,11 +2607,12 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(NTT > 48
             }
         }
     }
+    if constexpr (MODE == TC_PLAIN) return;
     __shared__ double tot[NACC];
     if (!sp_reduce_last_rs<NMOM, TC_NTH>(acc, rb, tot)) return;
     for (int m = NMOM + threadIdx.x; m < NACC; m += TC_NTH) tot[m] = 0.0;   // q = 0: rq, qq vanish
     __syncthreads();
-    if (!PLAN) {
+    if (MODE == TC_GATH) {
         for (int m = threadIdx.x; m < NACC; m += TC_NTH) gath[rank * NACC + m] = tot[m];
         return;
     }
@@ -2668,6 +2674,8 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
 #define FOTO_TPAIR_SIZES(X) X(48) X(64)
 
 #define FOTO_TCOL_SIZES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(32)
+
+#include "foto_gauss.inc"
 
 static bool tcol_supported(int n) {
 #define FOTO_TCOL_CASE(NN) if (n == NN) return true;
@@ -2752,6 +2760,15 @@ struct SpecImpl {
     std::vector<void*> allocs;
     int nblocks = 0;
     double c0 = 0, c1 = 1;
+    // Gauss-compressed CG (cg_mode 3, foto_gauss.inc); gauss_active: the solve in flight uses it
+    bool gauss = false, gauss_active = false;
+    int gq_nblk = 0;
+    GqState* gq = nullptr;
+    GqState* hgq = nullptr;       // pinned: the header (K, status, conv, done, bn2, rn2)
+    GqNodes* gqn = nullptr;
+    double* gq_part = nullptr;    // gq_nblk histograms
+    double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
+    double* gq_tab = nullptr;
 
     // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
     // sharded always); the pass a plan finishes marks the solve done in its tail
@@ -2766,6 +2783,7 @@ struct SpecImpl {
         for (void* p : allocs) (void)hipFree(p);
         if (hS) (void)hipHostFree(hS);
         if (hS2) (void)hipHostFree(hS2);
+        if (hgq) (void)hipHostFree(hgq);
     }
     SpecTab tab() const {
         SpecTab T;
@@ -2804,7 +2822,17 @@ static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, s
 
 static int reset_s2(SpecImpl* P, hipStream_t s);
 
+static int cus_count() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess) return cus;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+    return cus;
+}
+
 int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, int sstep, hipStream_t s) {
+    // cg_mode 3: the Gauss-compressed CG, with the s-step machinery kept for the (rare) redo
+    const bool gauss = (sstep == 3);
+    if (gauss) sstep = 2;
     if (sstep != 1 && sstep != 2) {
         set_error("spectral CG: s-step must be 1 or 2");
         return FOTO_ERR_ARG;
@@ -2943,6 +2971,19 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS2, sizeof(SStep)));
     FOTO_TRY(reset_s2(P, s));   // c0, c1 for the fused INIT (solve_tcol)
+    P->gauss = gauss;
+    if (gauss) {
+        // histogram blocks: one per CU (each holds 4 private 32 KB histograms), at most one per 4 rows
+        P->gq_nblk = std::max(1, std::min(cus_count(), (rows + 3) / 4));
+        FOTO_TRY(P->alloc(sizeof(GqState), &b)); P->gq = (GqState*)b;
+        FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
+        FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq, sizeof(GqState)));
+        FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
+        FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * P->gq_nblk, &b)); P->gq_part = (double*)b;
+        FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
+        FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    }
     return 0;
 }
 
@@ -3082,32 +3123,39 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
 
 // plan (forward): single shard, the kernel plans the first pass; sharded, it leaves this rank's INIT
 // moments in gath for the all-gather
+// inv: x^ = (b^ - r^)/lam (s-step) or, with P->gauss, Q(lam) b^ from the Gauss-compressed CG's table
 static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* out, double rtol, int maxiter,
-                              hipStream_t s, bool plan = true) {
+                              hipStream_t s, int mode = TC_PLAN) {
     const SpecTab T = P->tab();
     const int nb = P->tcol_nb;
+    const bool gq = inv && P->gauss_active;
+#define FOTO_TCOL_FWD(NN, K, M) K<NN, M><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter, \
+                                                                P->gath, P->rank)
 #define FOTO_TCOL_LAUNCH(NN)                                                                                       \
     if (P->g.Nt == NN) {                                                                                           \
-        if (inv) k_dct_t_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);                  \
-        else if (plan) k_dct_t_fwd_init<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol,  \
-                                                                      maxiter, P->gath, P->rank);                  \
-        else k_dct_t_fwd_init<NN, false><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter,  \
-                                                               P->gath, P->rank);                                  \
+        if (gq) k_dct_t_inv_q<NN><<<nb, TC_NTH, GQ_TAB_BYTES, s>>>(T, P->Cth, P->bh, P->gq_tab, P->gq, P->c0,      \
+                                                                    1.0 / P->c1, out);                             \
+        else if (inv) k_dct_t_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);             \
+        else if (mode == TC_PLAN) FOTO_TCOL_FWD(NN, k_dct_t_fwd_init, TC_PLAN);                                    \
+        else if (mode == TC_GATH) FOTO_TCOL_FWD(NN, k_dct_t_fwd_init, TC_GATH);                                    \
+        else FOTO_TCOL_FWD(NN, k_dct_t_fwd_init, TC_PLAIN);                                                        \
         return hipGetLastError();                                                                                  \
     }
     FOTO_TCOL_SIZES(FOTO_TCOL_LAUNCH)
 #undef FOTO_TCOL_LAUNCH
 #define FOTO_TPAIR_LAUNCH(NN)                                                                                      \
     if (P->g.Nt == NN) {                                                                                           \
-        if (inv) k_dct_tp_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);                 \
-        else if (plan) k_dct_tp_fwd_init<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, \
-                                                                       maxiter, P->gath, P->rank);                 \
-        else k_dct_tp_fwd_init<NN, false><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter, \
-                                                                P->gath, P->rank);                                 \
+        if (gq) k_dct_tp_inv_q<NN><<<nb, TC_NTH, GQ_TAB_BYTES, s>>>(T, P->Cth, P->bh, P->gq_tab, P->gq, P->c0,     \
+                                                                     1.0 / P->c1, out);                            \
+        else if (inv) k_dct_tp_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);            \
+        else if (mode == TC_PLAN) FOTO_TCOL_FWD(NN, k_dct_tp_fwd_init, TC_PLAN);                                   \
+        else if (mode == TC_GATH) FOTO_TCOL_FWD(NN, k_dct_tp_fwd_init, TC_GATH);                                   \
+        else FOTO_TCOL_FWD(NN, k_dct_tp_fwd_init, TC_PLAIN);                                                       \
         return hipGetLastError();                                                                                  \
     }
     FOTO_TPAIR_SIZES(FOTO_TPAIR_LAUNCH)
 #undef FOTO_TPAIR_LAUNCH
+#undef FOTO_TCOL_FWD
     return hipErrorNotSupported;
 }
 
@@ -3121,6 +3169,78 @@ static int tcol_inverse(SpecImpl* P, double* b, double* x, double rtol, int maxi
     FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, P->tmp, x, s));
     if (kt) kt->stop(e, s, FOTO_K_DCT, 7.0 * 8.0 * N);
     return 0;
+}
+
+// ---------------------------------------------------------------------------- Gauss-compressed CG (host)
+// b^ -> this box's histogram (slot rank of gq_hist)
+static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
+    const SpecTab T = P->tab();
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    k_gq_hist<<<P->gq_nblk, GQ_HNTH, 0, s>>>(T, P->bh, P->c0, 1.0 / P->c1, P->gq_part);
+    FOTO_HIP_CHECK(hipGetLastError());
+    k_gq_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_part, P->gq_nblk, P->gq_hist + (size_t)P->rank * GQ_HIST);
+    FOTO_HIP_CHECK(hipGetLastError());
+    if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
+    return 0;
+}
+
+// the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
+static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    k_gq_nodes<<<GQ_NODES / 256, 256, 0, s>>>(P->gq_hist, P->world, P->c0, P->c1, P->gqn);
+    FOTO_HIP_CHECK(hipGetLastError());
+    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, P->gq);
+    FOTO_HIP_CHECK(hipGetLastError());
+    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->c0, P->c1, P->gq_tab);
+    FOTO_HIP_CHECK(hipGetLastError());
+    if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq, P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
+    P->gauss_active = true;
+    return 0;
+}
+
+// x^ = Q(lam) b^ into the box layout the non-column inverse path expects (tmp)
+static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
+    const SpecTab T = P->tab();
+    const int nb = std::max(1, std::min(2048, (P->g.Nt * P->nyl + 3) / 4));
+    k_gq_xhat<<<nb, 256, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->c0, 1.0 / P->c1, out);
+    return hipGetLastError();
+}
+
+// single shard: b (physical, clobbered) -> b^ -> measure -> CG -> x, all enqueued
+static int gq_enqueue(SpecImpl* P, double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    const Geo& g = P->g;
+    const double N = (double)g.Nt * (double)g.nxy;
+    if (P->tcol) {
+        hipEvent_t e = kt ? kt->start(s) : nullptr;
+        FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
+        FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, b, s));
+        FOTO_HIP_CHECK(launch_tcol(P, false, b, nullptr, rtol, maxiter, s, TC_PLAIN));
+        if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    } else {
+        FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
+    }
+    FOTO_TRY(gq_measure(P, kt, s));
+    FOTO_TRY(gq_solve(P, rtol, maxiter, kt, s));
+    if (P->tcol) return tcol_inverse(P, b, x, rtol, maxiter, kt, s);   // launch_tcol: the Q kernel
+    FOTO_HIP_CHECK(gq_xhat(P, P->tmp, s));
+    return inverse3(P, P->tmp, b, x, kt, s);
+}
+
+// the s-step CG from b^ (still intact) when the tables could not represent the solve
+static int gq_redo(SpecImpl* P, double* b, double* x, double rtol, int maxiter, int* iters, int* info, KTimer* kt,
+                   hipStream_t s) {
+    P->gauss_active = false;
+    FOTO_TRY(solve_s2(P, rtol, maxiter, 0, iters, info, kt, s, false));
+    if (P->tcol) return tcol_inverse(P, b, x, rtol, maxiter, kt, s);
+    FOTO_HIP_CHECK(launch_xhat(P, s));
+    return inverse3(P, P->tmp, b, x, kt, s);
+}
+
+// after the stream has passed gq_solve's header copy
+static void gq_result(const SpecImpl* P, int maxiter, int* iters, int* info) {
+    *iters = P->hgq->K;
+    *info = P->hgq->conv ? 0 : maxiter;
 }
 
 // single shard, s-step, column-kernel t axis: b -x-> tmp -y-> b -t(+INIT)-> b^; CG passes;
@@ -3142,16 +3262,29 @@ static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxite
 
 bool SpectralPlan::deferrable() const {
     const SpecImpl* P = (const SpecImpl*)impl;
+    if (P->gauss) return P->world == 1;   // fixed work: nothing to predict
     return P->tcol && P->sstep == 2 && P->world == 1 && P->last_passes > 0;
 }
 
-const int* SpectralPlan::done_flag() const { return &((const SpecImpl*)impl)->S2->done; }
+const int* SpectralPlan::done_flag() const {
+    const SpecImpl* P = (const SpecImpl*)impl;
+    return P->gauss ? &P->gq->done : &P->S2->done;
+}
 
 int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     if (!deferrable() || P->pending) {
         set_error("spectral CG: deferred solve needs a single-shard s-step plan after a finished solve");
         return FOTO_ERR_STATE;
+    }
+    if (P->gauss) {
+        FOTO_TRY(gq_enqueue(P, b, x, rtol, maxiter, kt, s));
+        P->pending = true;
+        P->pend_b = b;
+        P->pend_x = x;
+        P->pend_rtol = rtol;
+        P->pend_maxiter = maxiter;
+        return 0;
     }
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
@@ -3189,6 +3322,15 @@ int SpectralPlan::finish(int* iters, int* info, int* redo, KTimer* kt, hipStream
     }
     P->pending = false;
     *redo = 0;
+    if (P->gauss) {
+        if (P->hgq->status != 0) {   // K beyond the table or a breakdown: the s-step CG from b^
+            *redo = 1;
+            return gq_redo(P, P->pend_b, P->pend_x, P->pend_rtol, P->pend_maxiter, iters, info, kt, s);
+        }
+        gq_result(P, P->pend_maxiter, iters, info);
+        P->gauss_active = false;
+        return 0;
+    }
     int passes = P->pend_launched;
     if (!P->hS2->done) {   // the predicted passes were not enough: continue, polling, and redo x
         *redo = 1;
@@ -3222,6 +3364,14 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     const SpecTab T = P->tab();
     const double N = (double)g.Nt * (double)g.nxy;
     const bool vec = P->vec();
+    if (P->gauss) {
+        FOTO_TRY(gq_enqueue(P, b, x, rtol, maxiter, kt, s));
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        if (P->hgq->status != 0) return gq_redo(P, b, x, rtol, maxiter, iters, info, kt, s);
+        gq_result(P, maxiter, iters, info);
+        P->gauss_active = false;
+        return 0;
+    }
     if (P->tcol) return solve_tcol(P, b, x, rtol, maxiter, predicted, iters, info, kt, s);
     // b (physical) -> b^ ; b is scratch afterwards
     FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
@@ -3283,7 +3433,7 @@ int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     if (P->tcol)   // box tmp -> b^ and this rank's INIT moments -> gath (cg_begin then launches nothing)
-        FOTO_HIP_CHECK(launch_tcol(P, false, P->tmp, nullptr, 0.0, 0, s, false));
+        FOTO_HIP_CHECK(launch_tcol(P, false, P->tmp, nullptr, 0.0, 0, s, P->gauss ? TC_PLAIN : TC_GATH));
     else
         FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, P->nyl * g.Nx, P->tmp, P->bh, s));   // box tmp -> b^
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
@@ -3292,7 +3442,7 @@ int SpectralPlan::fwd_t(KTimer* kt, hipStream_t s) {
 
 int SpectralPlan::cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
-    if (P->tcol) return 0;   // the column kernel of fwd_t took the INIT moments
+    if (P->tcol && !P->gauss) return 0;   // the column kernel of fwd_t took the INIT moments
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(launch_s2(P, true, rtol, maxiter, P->gath, s));
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 16.0 * P->nbox());
@@ -3338,7 +3488,8 @@ int SpectralPlan::inv_t(KTimer* kt, hipStream_t s) {
         if (kt) kt->stop(e, s, FOTO_K_DCT, 3.0 * 8.0 * P->nbox());
         return 0;
     }
-    FOTO_HIP_CHECK(launch_xhat(P, s));                                              // tmp = x^
+    if (P->gauss_active) FOTO_HIP_CHECK(gq_xhat(P, P->tmp, s));                     // tmp = x^
+    else FOTO_HIP_CHECK(launch_xhat(P, s));
     FOTO_HIP_CHECK(dct_pass(P, 2, true, 1, P->nyl * g.Nx, P->tmp, P->rh, s));    // rh = box of x~
     if (kt) kt->stop(e, s, FOTO_K_DCT, 2.0 * 8.0 * P->nbox());
     return 0;
@@ -3358,9 +3509,32 @@ int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t 
     return 0;
 }
 
+bool SpectralPlan::gauss() const { return ((const SpecImpl*)impl)->gauss; }
+int SpectralPlan::gauss_hist_size() { return GQ_HIST; }
+double* SpectralPlan::gauss_hist() const { return ((const SpecImpl*)impl)->gq_hist; }
+
+int SpectralPlan::gauss_measure(KTimer* kt, hipStream_t s) { return gq_measure((SpecImpl*)impl, kt, s); }
+
+int SpectralPlan::gauss_solve(double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+    return gq_solve((SpecImpl*)impl, rtol, maxiter, kt, s);
+}
+
+int SpectralPlan::gauss_wait(int maxiter, int* ok, int* iters, int* info, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    *ok = P->hgq->status == 0;
+    gq_result(P, maxiter, iters, info);
+    if (!*ok) P->gauss_active = false;
+    return 0;
+}
+
+void SpectralPlan::gauss_end() { ((SpecImpl*)impl)->gauss_active = false; }
+
 int SpectralPlan::reset(hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     P->pending = false;
+    P->gauss_active = false;
+    if (P->gq) FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
     P->pend_launched = 0;
     P->last_passes = 0;
     FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));

@@ -18,6 +18,7 @@ from ._lib import check, dptr, f64, lib
 CG_STENCIL = 0
 CG_SPECTRAL = 1
 CG_SSTEP = 2
+CG_GAUSS = 3
 
 
 class BBSolver:

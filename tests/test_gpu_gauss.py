@@ -1,0 +1,85 @@
+"""Gauss-compressed spectral CG (cg_mode 3, csrc/foto_gauss.inc) against the oracle's scipy CG,
+the stencil CG (mode 0) and the s-step CG (mode 2).
+
+Bars (tests/test_gpu_parity.py's CG bar): iteration count within +-1 of the oracle and
+max|x - x_oracle| <= 1e-8 max|x_oracle|; full BB solves: crit within 1e-5 relative of mode 2,
+CG counts within +-1, flow within 1e-5 px.  The numpy feasibility study
+(tools/gautschi_proto.py) puts the compressed measure's residual norms within 1.5e-13 of the
+literal CG and x within 2e-14 of scipy's, so the bars have wide margins.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+foto = pytest.importorskip("foto")
+from foto import ops  # noqa: E402
+from foto.bb import BBSolver  # noqa: E402
+from foto.synthetic import translating_gaussian  # noqa: E402
+from oracle import foto_oracle as O  # noqa: E402
+
+
+def _first_rhs(Nt, Nx, Ny, r=1.0):
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    N, nxy = Nt * Nx * Ny, Nx * Ny
+    mu = np.zeros(3 * N)
+    for n in range(Nt):
+        mu[n * nxy:(n + 1) * nxy] = (1 - n / (Nt - 1)) * rho0 + (n / (Nt - 1)) * rhoT
+    return O.bb_rhs(mu, np.zeros(3 * N), rho0, rhoT, r, Nt, Ny, Nx)
+
+
+@pytest.mark.parametrize("Nt,Nx,Ny,eps", [
+    (8, 48, 40, 1e-2),      # column kernel t axis
+    (16, 80, 60, 1e-2),
+    (32, 80, 60, 1e-3),     # harder: ~280 iterations
+    (12, 50, 34, 1e-2),     # odd-ish sizes
+    (7, 30, 22, 1e-2),      # no column kernel (odd Nt): x^ kernel + t-DCT pass
+])
+def test_gauss_cg_vs_oracle(Nt, Nx, Ny, eps):
+    F = _first_rhs(Nt, Nx, Ny)
+    xo, io, ko = O.cg(O.assemble_A(1.0, eps, Nt, Ny, Nx).dot, F)
+    sc = np.abs(xo).max()
+    for mode in (0, 2, 3):
+        x, info, k = ops.cg(F, Nt, Nx, Ny, 1.0, eps, mode=mode)
+        err = np.abs(x - xo).max() / sc
+        print(f"{Nt}x{Nx}x{Ny} eps {eps:g} mode {mode}: {k} its (oracle {ko}), info {info}, err {err:.2e}")
+        assert info == io == 0
+        assert abs(k - ko) <= 1, (mode, k, ko)
+        assert err <= 1e-8, (mode, err)
+
+
+def test_gauss_cg_edge_cases():
+    Nt, Nx, Ny = 8, 24, 20
+    # b = 0: zero iterations, x = 0 (scipy returns at once)
+    x, info, k = ops.cg(np.zeros(Nt * Nx * Ny), Nt, Nx, Ny, 1.0, 1e-2, mode=3)
+    assert k == 0 and info == 0 and not np.any(x)
+    # maxiter reached: the iterate after maxiter steps, info = maxiter
+    F = _first_rhs(Nt, Nx, Ny)
+    xo, io, ko = O.cg(O.assemble_A(1.0, 1e-2, Nt, Ny, Nx).dot, F, maxiter=5)
+    x, info, k = ops.cg(F, Nt, Nx, Ny, 1.0, 1e-2, maxiter=5, mode=3)
+    assert (info, k) == (5, 5) and io == 5
+    assert np.abs(x - xo).max() <= 1e-10 * np.abs(xo).max()
+    # beyond the solution table (maxiter > K_MAX with eps tiny): the s-step redo, same answer
+    xo, io, ko = O.cg(O.assemble_A(1.0, 1e-5, Nt, Ny, Nx).dot, F, maxiter=1000)
+    x, info, k = ops.cg(F, Nt, Nx, Ny, 1.0, 1e-5, mode=3)
+    print("eps 1e-5:", k, ko, info, io)
+    assert abs(k - ko) <= 1 and info == io
+
+
+@pytest.mark.parametrize("Nt,Nx,Ny,vr", [(16, 96, 80, 1), (16, 96, 80, 3), (32, 640, 480, 1)])
+def test_gauss_bb_solve_vs_sstep(Nt, Nx, Ny, vr):
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = {}
+    for mode in (2, 3):
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode, virtual_ranks=vr) as s:
+            s.iterate(8, 0.0, stop_rules=False)
+            u, v, m = s.flow()
+            out[mode] = (np.array(s.crit), np.array(s.cg_its), u, v, s.stats())
+    c2, k2, u2, v2, _ = out[2]
+    c3, k3, u3, v3, st3 = out[3]
+    print("crit rel", np.max(np.abs(c3 - c2) / np.abs(c2)), "CG", k2, k3, "u", np.abs(u3 - u2).max(),
+          "redo", st3["cg_redo"])
+    assert np.max(np.abs(c3 - c2) / np.abs(c2)) <= 1e-5
+    assert np.abs(k3 - k2).max() <= 1
+    assert np.abs(u3 - u2).max() <= 1e-5 and np.abs(v3 - v2).max() <= 1e-5
+    assert st3["cg_redo"] == 0
