@@ -40,8 +40,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "2")),
-                    help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG (default)")
+    ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "3")),
+                    help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG, 3 Gauss-compressed spectral CG (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn", action="store_true", help="skip the GN (classical.py, config 3) side measurement")
     ap.add_argument("--no-stencil", action="store_true", help="skip the literal stencil-CG side measurement")

@@ -79,10 +79,10 @@ typedef struct {
     double cg_rtol;       /* 1e-6 (benamou_brenier.py:85)                                  */
     int cg_mode;          /* 0 = stencil CG (7-point matvec), 1 = spectral CG (DCT-II      */
                           /* eigenbasis, one pass / iteration), 2 = spectral s-step CG     */
-                          /* (default; one pass / up to 8 iterations, any world; mode 1    */
-                          /* needs world == 1; eps <= 0 selects mode 0), 3 = spectral CG   */
-                          /* on the Gauss-compressed measure of b^ (one read of b^, the    */
-                          /* recurrence on 2048 nodes; any world)                          */
+                          /* (one pass / up to 8 iterations, any world; mode 1 needs       */
+                          /* world == 1; eps <= 0 selects mode 0), 3 = spectral CG on the  */
+                          /* Gauss-compressed measure of b^ (default: one read of b^, the  */
+                          /* recurrence on 2048 nodes, any world)                          */
     int rank, world;      /* time-slab sharding over `world` processes (RCCL); 1 = single  */
     const void* nccl_id;  /* 128-byte ncclUniqueId (foto_nccl_unique_id on rank 0)         */
     int virtual_ranks;    /* >1: shard over this many in-process slabs on ONE device       */

@@ -3,9 +3,10 @@
 ``solve`` keeps the signature, defaults, stdout and return value of the reference
 (benamou_brenier.py:151-271); the whole outer loop (RHS, Poisson CG, projection, multiplier
 update, criterion) and the flow extraction run in libfoto.so (HIP, gfx950).  The Poisson CG
-is selected by ``cg_mode`` (env FOTO_CG_MODE): 2 = s-step CG in the DCT-II eigenbasis of A
-(default), 1 = one-pass CG in that basis, 0 = 7-point stencil CG (also the time-sharded
-multi-GPU path).  All three follow scipy's CG recurrence and stopping rule.
+is selected by ``cg_mode`` (env FOTO_CG_MODE): 3 = CG on the Gauss-compressed spectral
+measure of the right-hand side (default; csrc/foto_gauss.inc), 2 = s-step CG in the DCT-II
+eigenbasis of A, 1 = one-pass CG in that basis, 0 = 7-point stencil CG.  All follow scipy's
+CG recurrence and stopping rule; every mode runs time-sharded over GPUs.
 """
 import os
 
@@ -16,7 +17,7 @@ from foto import ops as _ops
 
 
 def _default_mode():
-    return int(os.environ.get("FOTO_CG_MODE", "2"))
+    return int(os.environ.get("FOTO_CG_MODE", "3"))
 
 
 def solve_benamou_brenier_step(mu, q, rho0, rhoT, r, A, div, Nt, Nx, Ny, dt, dx, dy):

@@ -662,7 +662,7 @@ int foto_bb_opts_default(foto_bb_opts* o) {
     o->device = -1;
     o->cg_maxiter = 1000;
     o->cg_rtol = 1e-6;
-    o->cg_mode = 2;   // spectral s-step CG (falls back to the stencil CG when eps <= 0)
+    o->cg_mode = 3;   // Gauss-compressed spectral CG (falls back to the stencil CG when eps <= 0)
     o->rank = 0;
     o->world = 1;
     o->nccl_id = nullptr;

@@ -2979,7 +2979,8 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
         FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq, sizeof(GqState)));
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
-        FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * P->gq_nblk, &b)); P->gq_part = (double*)b;
+        const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;   // + the first reduction level
+        FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * (P->gq_nblk + ngroups), &b)); P->gq_part = (double*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
         FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
@@ -3178,7 +3179,11 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     k_gq_hist<<<P->gq_nblk, GQ_HNTH, 0, s>>>(T, P->bh, P->c0, 1.0 / P->c1, P->gq_part);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_part, P->gq_nblk, P->gq_hist + (size_t)P->rank * GQ_HIST);
+    const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;
+    double* grp = P->gq_part + (size_t)P->gq_nblk * GQ_HIST;
+    k_gq_reduce1<<<ngroups * GQ_HIST / 256, 256, 0, s>>>(P->gq_part, P->gq_nblk, grp);
+    FOTO_HIP_CHECK(hipGetLastError());
+    k_gq_reduce2<<<GQ_HIST / 256, 256, 0, s>>>(grp, ngroups, P->gq_hist + (size_t)P->rank * GQ_HIST);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
     return 0;
@@ -3187,7 +3192,7 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
 // the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
 static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_gq_nodes<<<GQ_NODES / 256, 256, 0, s>>>(P->gq_hist, P->world, P->c0, P->c1, P->gqn);
+    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->world, P->c0, P->c1, P->gqn);
     FOTO_HIP_CHECK(hipGetLastError());
     k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, P->gq);
     FOTO_HIP_CHECK(hipGetLastError());
@@ -3203,7 +3208,7 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
 static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
     const SpecTab T = P->tab();
     const int nb = std::max(1, std::min(2048, (P->g.Nt * P->nyl + 3) / 4));
-    k_gq_xhat<<<nb, 256, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->c0, 1.0 / P->c1, out);
+    k_gq_xhat<<<nb, 256, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->c0, 1.0 / P->c1, out);
     return hipGetLastError();
 }
 

@@ -26,15 +26,16 @@ class BBSolver:
 
     Parameters mirror ``benamou_brenier.solve``; ``cg_mode`` picks the Poisson CG
     (0 = the literal 7-point stencil CG, 1 = the same CG run in the DCT-II eigenbasis of A,
-    2 = that spectral CG in s-step passes of up to 8 iterations -- the default, as in the C
-    ABI's foto_bb_opts_default and the drop-in benamou_brenier.solve);
+    2 = that spectral CG in s-step passes of up to 8 iterations, 3 = scipy's CG recurrence on
+    the Gauss-compressed spectral measure of b -- the default, as in the C ABI's
+    foto_bb_opts_default and the drop-in benamou_brenier.solve);
     ``rank/world/nccl_id`` shard the time axis over processes (RCCL),
     ``virtual_ranks`` shards it in-process on one device (test path); ``library`` is a
     ``_lib.load``-ed build other than the product libfoto.so (tests).
     """
 
     def __init__(self, rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-3, *, device=-1, cg_rtol=1e-6,
-                 cg_maxiter=1000, cg_mode=CG_SSTEP, rank=0, world=1, nccl_id=None, virtual_ranks=1,
+                 cg_maxiter=1000, cg_mode=CG_GAUSS, rank=0, world=1, nccl_id=None, virtual_ranks=1,
                  timing=False, library=None):
         self._L = library if library is not None else lib()
         Nt, Nx, Ny = int(Nt), int(Nx), int(Ny)

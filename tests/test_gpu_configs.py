@@ -49,7 +49,7 @@ def _true_residual_ok(s, mu, q, rho0, rhoT, Nt, Nx, Ny, r, eps):
     return res / np.linalg.norm(F)
 
 
-@pytest.mark.parametrize("mode", [2, 0])
+@pytest.mark.parametrize("mode", [3, 2, 0])
 def test_metric_grid_vs_reference(gold, mode):
     d = gold("bb_metric.npz")
     Nt, Ny, Nx = (int(v) for v in d["shape"])
@@ -74,7 +74,8 @@ def test_metric_grid_vs_reference(gold, mode):
         assert err <= 1e-7
 
 
-def test_metric_grid_true_residual_ten_outer():
+@pytest.mark.parametrize("mode", [3, 2])
+def test_metric_grid_true_residual_ten_outer(mode):
     """The default path (spectral s-step CG: deferred, late-planned passes, the interval
     adapted from the previous right-hand side) solves A phi = F to scipy's rule on every
     outer iteration, not just the first: ||F - A phi|| <= 1.01 rtol ||F|| for ten outer
@@ -82,7 +83,7 @@ def test_metric_grid_true_residual_ten_outer():
     (which enqueues each next RHS before waiting: the early-head path)."""
     Nt, Nx, Ny, r, eps = 32, 640, 480, 1.0, 1e-2
     rho0, rhoT = translating_gaussian(Nx, Ny)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
         for i in range(10):
             mu, q = s.state()
             s.iterate(1, 0.0, False)
@@ -90,13 +91,13 @@ def test_metric_grid_true_residual_ten_outer():
             print(f"outer {i + 1}: cg {s.cg_its[-1]}, true residual {rel:.3e} of ||F||")
             assert rel <= 1.01 * RTOL_CG
         crit_steps = np.array(s.crit)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode) as s:
         s.iterate(10, 0.0, False)
         crit_one = np.array(s.crit)
     np.testing.assert_allclose(crit_one, crit_steps, rtol=1e-9, atol=0)
 
 
-@pytest.mark.parametrize("mode", [2, 0])
+@pytest.mark.parametrize("mode", [3, 2, 0])
 def test_c2_shape_vs_reference(gold, mode):
     d = gold("bb_c2s.npz")
     Nt, Ny, Nx = (int(v) for v in d["shape"])
@@ -169,10 +170,11 @@ def test_c4_full_size():
     Nt, Nx, Ny, r, eps = 64, 1024, 1024, 1.0, 1e-2
     rho0, rhoT = translating_gaussian(Nx, Ny)
     out = {}
-    for key, mode, vr in (("spectral", 2, 1), ("stencil", 0, 1), ("spectral x8", 2, 8)):
+    for key, mode, vr in (("spectral", 2, 1), ("stencil", 0, 1), ("spectral x8", 2, 8), ("gauss", 3, 1),
+                          ("gauss x8", 3, 8)):
         with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode, virtual_ranks=vr) as s:
             rels = []
-            if vr == 1 and mode == 2:
+            if vr == 1 and mode in (2, 3):
                 for _ in range(2):
                     mu, q = s.state()
                     s.iterate(1, 0.0, False)
@@ -191,3 +193,12 @@ def test_c4_full_size():
     assert _rel(p2, p0) <= 1e-8
     np.testing.assert_allclose(c8, c2, rtol=1e-7)
     assert _rel(p8, p2) <= 1e-6
+    # the Gauss-compressed CG (cg_mode 3), one shard and eight, against the s-step CG
+    (k3, c3, p3, r3), (k38, c38, p38, _) = out["gauss"], out["gauss x8"]
+    print(f"C4 gauss cg {k3.tolist()} x8 {k38.tolist()}; vs s-step crit rel {_rel(c3, c2):.2e} phi rel "
+          f"{_rel(p3, p2):.2e}; x8 vs one crit rel {_rel(c38, c3):.2e}; true residuals {r3}")
+    assert max(r3) <= 1.01 * RTOL_CG
+    assert np.max(np.abs(k3 - k2)) <= 1 and np.max(np.abs(k38 - k3)) <= 1
+    np.testing.assert_allclose(c3, c2, rtol=1e-7)
+    assert _rel(p3, p2) <= 1e-8
+    np.testing.assert_allclose(c38, c3, rtol=1e-7)

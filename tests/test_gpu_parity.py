@@ -85,7 +85,7 @@ def test_bb_rhs(gold):
     np.testing.assert_allclose(F, d["F"], rtol=0, atol=1e-13)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_cg(gold, mode):
     d = gold("cg.npz")
     for c in range(3):
@@ -104,7 +104,7 @@ def test_cg(gold, mode):
         np.testing.assert_allclose(x5, d[f"c{c}_x_max5"], rtol=0, atol=1e-10 * np.abs(d[f"c{c}_x_max5"]).max())
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("Nt", [4, 5])   # mode 2: Nt = 4 takes the fused t-axis column kernels, 5 the GEMM path
 def test_cg_zero_iterations(mode, Nt):
     """No CG iteration runs (b = 0, or maxiter = 0): x = x0 = 0 exactly, as scipy returns."""
@@ -136,7 +136,7 @@ def test_flow(gold):
         np.testing.assert_allclose(m, d[f"f{f}_m"], rtol=1e-13, atol=1e-12)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("name", ["bb_small.npz", "bb_tex.npz"])
 def test_bb_solve_small(gold, name, mode, capsys):
     d = gold(name)
@@ -158,7 +158,7 @@ def test_bb_solve_small(gold, name, mode, capsys):
 
 def test_bb_solve_c_entry_default(gold):
     """foto_bb_solve, the one-shot C entry the INTEGRATION.md ctypes binding calls, at its
-    default CG (spectral s-step) matches the reference's golden solve; reg_epsilon = 0 falls
+    default CG (the Gauss-compressed spectral CG) matches the reference's golden solve; reg_epsilon = 0 falls
     back to the stencil CG instead of failing (the spectral CGs divide by lam = r eps + ...)."""
     import ctypes
     from foto import _lib
@@ -182,7 +182,7 @@ def test_bb_solve_c_entry_default(gold):
     assert np.all(np.isfinite(u)) and np.all(np.isfinite(v))
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_bb_solve_c1(gold, mode):
     d = gold("bb_c1.npz")
     Nt, Ny, Nx = (int(s) for s in d["shape"])
@@ -255,7 +255,7 @@ def test_bb_cg_maxiter_deferred(gold, monkeypatch):
     np.testing.assert_allclose(res["s2"][0], res["s1"][0], rtol=1e-8, atol=0)
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 3])
 @pytest.mark.parametrize("vr", [2, 3, 5])
 def test_bb_virtual_ranks_match_single(gold, vr, mode):
     """The time-sharded path on one device with `vr` in-process shards reproduces the
@@ -300,7 +300,7 @@ def test_bb_solver_state_and_stats(gold):
         assert st["kernels"]["cg_dir"]["n"] <= st["cg_iters_total"] + 3 * 8
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 3])
 @pytest.mark.parametrize("name", ["bb_tex.npz", "bb_c1.npz"])
 def test_bb_fused_prox_rhs_matches_separate(gold, monkeypatch, name, mode):
     """The single-shard default fuses stepB / stepC / crit with the next iteration's RHS
@@ -406,7 +406,7 @@ def test_full_size_spectral_matches_stencil():
     Nt, Ny, Nx = 32, 480, 640
     rho0, rhoT = translating_gaussian(Nx, Ny)
     out = []
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 3):
         with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
             s.iterate(2, 0.0, False)
             out.append((np.array(s.cg_its), np.array(s.crit), s.phi()))
@@ -417,8 +417,9 @@ def test_full_size_spectral_matches_stencil():
         np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6 * np.abs(p0).max())
 
 
+@pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("nv", [4, 8])
-def test_full_size_sharded_spectral_matches_single(nv):
+def test_full_size_sharded_spectral_matches_single(nv, mode):
     """Bench grid, nv in-process shards of the spectral s-step CG vs one shard (nv = 8: the
     decomposition `bench.py --gpus 8` runs -- 4 planes and 60 rows per rank -- through the
     same transfer lists RCCL executes)."""
@@ -427,7 +428,7 @@ def test_full_size_sharded_spectral_matches_single(nv):
     rho0, rhoT = translating_gaussian(Nx, Ny)
     out = []
     for vr in (1, nv):
-        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2, virtual_ranks=vr) as s:
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode, virtual_ranks=vr) as s:
             s.iterate(2, 0.0, False)
             out.append((np.array(s.cg_its), np.array(s.crit), s.phi(), s.flow()))
     (k0, c0, p0, f0), (k1, c1, p1, f1) = out
@@ -438,11 +439,12 @@ def test_full_size_sharded_spectral_matches_single(nv):
         np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)
 
 
-def test_full_size_cg_true_residual():
+@pytest.mark.parametrize("mode", [2, 3])
+def test_full_size_cg_true_residual(mode):
     from foto.synthetic import translating_gaussian
     Nt, Ny, Nx = 32, 480, 640
     rho0, rhoT = translating_gaussian(Nx, Ny)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
         s.iterate(1, 0.0, False)
         phi = s.phi()
         assert 100 < s.cg_its[0] < 1000
@@ -454,7 +456,8 @@ def test_full_size_cg_true_residual():
     assert np.linalg.norm(res) <= 1.01e-6 * np.linalg.norm(F)
 
 
-def test_full_size_cg_true_residual_every_outer():
+@pytest.mark.parametrize("mode", [2, 3])
+def test_full_size_cg_true_residual_every_outer(mode):
     """Bench grid, outer iterations 1..10 of the default path (deferred late-planned ring
     passes, the interval adapted from the previous b^, the 3e4 cancellation limit): before
     every iterate(1) read (mu, q), rebuild F with the RHS kernel (benamou_brenier.py:64-82)
@@ -465,7 +468,7 @@ def test_full_size_cg_true_residual_every_outer():
     Nt, Ny, Nx, K = 32, 480, 640, 10
     rho0, rhoT = translating_gaussian(Nx, Ny)
     ratios = []
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
         for _ in range(K):
             mu, q = s.state()
             s.iterate(1, 0.0, False)
@@ -475,7 +478,7 @@ def test_full_size_cg_true_residual_every_outer():
         crit_chunked = np.array(s.crit)
     print("true residual / (rtol ||F||) per outer:", np.round(ratios, 4))
     assert max(ratios) <= 1.01, ratios
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=mode) as s:
         s.iterate(K, 0.0, False)
         np.testing.assert_allclose(np.array(s.crit), crit_chunked, rtol=1e-9)
 

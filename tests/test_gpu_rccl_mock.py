@@ -84,14 +84,17 @@ def compare(ranks, virt, Nt, Nx, Ny, W):
         assert ranks[g]["flow"] is None
 
 
+@pytest.mark.parametrize("cg_mode", [2, 3])
 @pytest.mark.parametrize("W", [2, 3, 5, 8])
-def test_rccl_path_bit_identical_to_virtual_ranks(W):
+def test_rccl_path_bit_identical_to_virtual_ranks(W, cg_mode):
+    """cg_mode 2: one moment all-gather per s-step pass; cg_mode 3: one histogram all-gather
+    (4096 doubles) per CG solve."""
     from foto.synthetic import translating_gaussian
     Nt, Nx, Ny = 16, 64, 48
     rho0, rhoT = translating_gaussian(Nx, Ny)
     L = _mock()
-    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6)
-    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6)
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6, cg_mode=cg_mode)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=6, cg_mode=cg_mode)
     compare(ranks, virt, Nt, Nx, Ny, W)
 
 
@@ -106,7 +109,8 @@ def test_rccl_path_stencil_cg():
     compare(ranks, virt, Nt, Nx, Ny, W)
 
 
-def test_rccl_path_bench_grid_w8():
+@pytest.mark.parametrize("cg_mode", [2, 3])
+def test_rccl_path_bench_grid_w8(cg_mode):
     """The driver's 8-GPU scaling run: the bench grid 640x480x32 over 8 ranks (4 planes and 60
     rows each), three outer iterations, against the same decomposition as virtual ranks and,
     within the spectral path's bar, against one shard."""
@@ -114,9 +118,9 @@ def test_rccl_path_bench_grid_w8():
     Nt, Nx, Ny, W = 32, 640, 480, 8
     rho0, rhoT = translating_gaussian(Nx, Ny)
     L = _mock()
-    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3)
-    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3)
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=cg_mode)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=cg_mode)
     compare(ranks, virt, Nt, Nx, Ny, W)
-    one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=3)
+    one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=cg_mode)
     assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
     np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)
