@@ -2507,8 +2507,9 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
     sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
 }
 
-// Sg->k = iterations applied; 0: no pass ran, r^ was never written and r = b^ (x^ = 0)
-template <int NTT>
+// Sg->k = iterations applied; 0: no pass ran, r^ was never written and r = b^ (x^ = 0).
+// PLAIN: bh holds x^ itself (the Gauss-compressed CG's k_gq_xhat output); rh, Sg unused.
+template <int NTT, bool PLAIN = false>
 __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_WPE))) void k_dct_t_inv_xhat(SpecTab T, const double* __restrict__ Ch,
                                                            const double* __restrict__ bh, const double* __restrict__ rh,
                                                            const SStep* Sg, double* __restrict__ out) {
@@ -2516,7 +2517,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
     const int64_t ncols = (int64_t)T.nyl * T.Nx;
     const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
     if (c >= ncols) return;
-    if (Sg->k == 0) rh = bh;
+    if (!PLAIN && Sg->k == 0) rh = bh;
     const int kyl = (int)(c / T.Nx), kx = (int)(c - (int64_t)kyl * T.Nx), ky = T.y0 + kyl;
     double xe[H], xo[H];   // x^_{2m}, x^_{2m+1}
 #pragma unroll
@@ -2524,8 +2525,13 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int k = 2 * m + p;
-            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
-            const double v = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+            double v;
+            if constexpr (PLAIN) {
+                v = bh[k * ncols + c];
+            } else {
+                const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+                v = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+            }
             if (p == 0) xe[m] = v;
             else xo[m] = v;
         }
@@ -2621,7 +2627,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(NTT > 48
     sstep_plan_wave(Sg, S0, tot, xb, 1, rtol, maxiter);
 }
 
-template <int NTT>
+template <int NTT, bool PLAIN = false>
 __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_dct_tp_inv_xhat(
         SpecTab T, const double* __restrict__ Ch, const double* __restrict__ bh, const double* __restrict__ rh,
         const SStep* Sg, double* __restrict__ out) {
@@ -2632,7 +2638,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
     const int64_t c = ((int64_t)blockIdx.x * (TC_NTH / 128) + pair) * 64 + lane;
     const bool ok = c < ncols;
-    if (Sg->k == 0) rh = bh;   // no pass ran: r = b^, x^ = 0
+    if (!PLAIN && Sg->k == 0) rh = bh;   // no pass ran: r = b^, x^ = 0
     __shared__ double xs[TC_NTH / 128][2][TP_CH][64];   // [pair][role][row of chunk][column]
     double xk[H];   // x^_{2m + role}
     if (ok) {
@@ -2640,8 +2646,12 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
         for (int m = 0; m < H; ++m) {
             const int k = 2 * m + role;
-            const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
-            xk[m] = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+            if constexpr (PLAIN) {
+                xk[m] = bh[k * ncols + c];
+            } else {
+                const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
+                xk[m] = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
+            }
         }
     } else {
 #pragma unroll
@@ -2822,10 +2832,13 @@ static void dct_matrix(int n, std::vector<double>& C, std::vector<double>& CT, s
 
 static int reset_s2(SpecImpl* P, hipStream_t s);
 
-static int cus_count() {
+static int cus_count() {   // CUs of the current device (cached per device ordinal)
+    static int cache[64] = {0};
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess) return cus;
+    if (dev >= 0 && dev < 64 && cache[dev] > 0) return cache[dev];
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+    if (dev >= 0 && dev < 64) cache[dev] = cus;
     return cus;
 }
 
@@ -3124,18 +3137,31 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
 
 // plan (forward): single shard, the kernel plans the first pass; sharded, it leaves this rank's INIT
 // moments in gath for the all-gather
+// x^ = Q(lam) b^ (the Gauss-compressed CG's solution table) into a box buffer: one persistent
+// 1024-thread block per CU (the 64 KB table allows one)
+static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
+    const SpecTab T = P->tab();
+    const int rows = P->g.Nt * P->nyl;
+    const int nb = std::max(1, std::min(cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
+    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->c0, 1.0 / P->c1, out);
+    return hipGetLastError();
+}
+
 // inv: x^ = (b^ - r^)/lam (s-step) or, with P->gauss, Q(lam) b^ from the Gauss-compressed CG's table
 static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* out, double rtol, int maxiter,
                               hipStream_t s, int mode = TC_PLAN) {
     const SpecTab T = P->tab();
     const int nb = P->tcol_nb;
     const bool gq = inv && P->gauss_active;
+    if (gq) {   // x^ -> rh, then the plain inverse below
+        const hipError_t e = gq_xhat(P, P->rh, s);
+        if (e != hipSuccess) return e;
+    }
 #define FOTO_TCOL_FWD(NN, K, M) K<NN, M><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter, \
                                                                 P->gath, P->rank)
 #define FOTO_TCOL_LAUNCH(NN)                                                                                       \
     if (P->g.Nt == NN) {                                                                                           \
-        if (gq) k_dct_t_inv_q<NN><<<nb, TC_NTH, GQ_TAB_BYTES, s>>>(T, P->Cth, P->bh, P->gq_tab, P->gq, P->c0,      \
-                                                                    1.0 / P->c1, out);                             \
+        if (gq) k_dct_t_inv_xhat<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->rh, nullptr, nullptr, out);         \
         else if (inv) k_dct_t_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);             \
         else if (mode == TC_PLAN) FOTO_TCOL_FWD(NN, k_dct_t_fwd_init, TC_PLAN);                                    \
         else if (mode == TC_GATH) FOTO_TCOL_FWD(NN, k_dct_t_fwd_init, TC_GATH);                                    \
@@ -3146,8 +3172,7 @@ static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* o
 #undef FOTO_TCOL_LAUNCH
 #define FOTO_TPAIR_LAUNCH(NN)                                                                                      \
     if (P->g.Nt == NN) {                                                                                           \
-        if (gq) k_dct_tp_inv_q<NN><<<nb, TC_NTH, GQ_TAB_BYTES, s>>>(T, P->Cth, P->bh, P->gq_tab, P->gq, P->c0,     \
-                                                                     1.0 / P->c1, out);                            \
+        if (gq) k_dct_tp_inv_xhat<NN, true><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->rh, nullptr, nullptr, out);        \
         else if (inv) k_dct_tp_inv_xhat<NN><<<nb, TC_NTH, 0, s>>>(T, P->Cth, P->bh, P->rh, P->S2, out);            \
         else if (mode == TC_PLAN) FOTO_TCOL_FWD(NN, k_dct_tp_fwd_init, TC_PLAN);                                   \
         else if (mode == TC_GATH) FOTO_TCOL_FWD(NN, k_dct_tp_fwd_init, TC_GATH);                                   \
@@ -3204,13 +3229,6 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
     return 0;
 }
 
-// x^ = Q(lam) b^ into the box layout the non-column inverse path expects (tmp)
-static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
-    const SpecTab T = P->tab();
-    const int nb = std::max(1, std::min(2048, (P->g.Nt * P->nyl + 3) / 4));
-    k_gq_xhat<<<nb, 256, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->c0, 1.0 / P->c1, out);
-    return hipGetLastError();
-}
 
 // single shard: b (physical, clobbered) -> b^ -> measure -> CG -> x, all enqueued
 static int gq_enqueue(SpecImpl* P, double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {

@@ -23,7 +23,10 @@ import os
 
 SHORT = {
     # first match wins: the specific names before their prefixes
-    "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox": "prox", "k_rhs": "rhs",
+    "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox_rhs": "prox", "k_prox": "prox_sep", "k_rhs": "rhs",
+    "k_gq_hist": "gq_hist", "k_gq_reduce": "gq_reduce", "k_gq_nodes": "gq_nodes", "k_gq_cg": "gq_cg",
+    "k_gq_qtab": "gq_qtab", "k_gq_xhat": "gq_xhat", "k_dct_t_inv_q": "dct_t_q", "k_dct_tp_inv_q": "dct_tp_q",
+    "k_dct_tp_fwd_init": "dct_tp_init", "k_dct_tp_inv_xhat": "dct_tp_xhat",
     "k_spec_s2_plan": "spec_plan", "k_spec_s2": "spec_cg", "k_spec_init": "spec_init", "k_spec_xhat": "spec_xhat",
     "k_spec_cg": "spec_cg1", "k_dct_fft_fwd": "dct_fft_fwd", "k_dct_fft_inv": "dct_fft_inv",
     "k_dct_t_fwd_init": "dct_t_init", "k_dct_t_inv_xhat": "dct_t_xhat", "k_dct": "dct_gemm", "k_traj": "flow",
@@ -33,6 +36,7 @@ SHORT = {
 
 # bytes per lane of each hot kernel's streaming loads (csrc/*.hip)
 LOAD_WIDTH = {"spec_cg": 16, "spec_cg1": 16, "spec_init": 16, "spec_xhat": 16, "cg_upd": 8, "cg_dir": 8, "prox": 8,
+              "prox_sep": 8, "gq_hist": 16, "dct_t_q": 8, "dct_tp_q": 8, "dct_tp_init": 8, "dct_tp_xhat": 8,
               "rhs": 8, "dct_fft_fwd": 8, "dct_fft_inv": 8, "dct_t_init": 8, "dct_t_xhat": 8, "dct_gemm": 8, "flow": 8,
               "gn_dir": 8, "gn_upd": 8}
 CALIB_BYTES = {"rd8": 2 << 30, "rd16": 2 << 30, "wr8": 1 << 30, "wr16": 1 << 30}
