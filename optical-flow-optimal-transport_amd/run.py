@@ -217,31 +217,64 @@ def touch(path):
 
 
 class Writer:
-    """Output files on one background thread, in submission order (a marker is written after
-    the files of its solve); ``drain`` waits and re-raises the first failure."""
+    """Output files on background threads (PNG encoding releases the GIL, so a few threads
+    keep up with the GPU); ``when_all`` runs a function once a set of writes has finished
+    (a marker after the files of its solve); ``drain`` waits and re-raises the first failure."""
 
-    def __init__(self, threads=1):
+    def __init__(self, threads=4):
+        import threading
         from concurrent.futures import ThreadPoolExecutor
         self.pool = ThreadPoolExecutor(max_workers=threads) if threads > 0 else None
         self.futs = []
+        self.lock = threading.Lock()
+        self.errors = []
 
     def submit(self, fn, *a):
         if self.pool is None:
             fn(*a)
-        else:
-            self.futs.append(self.pool.submit(fn, *a))
+            return None
+        f = self.pool.submit(fn, *a)
+        self.futs.append(f)
+        return f
+
+    def when_all(self, futs, fn, *a):
+        """fn(*a) after every future in futs succeeded (at once when there are none)."""
+        futs = [f for f in futs if f is not None]
+        if not futs:
+            fn(*a)
+            return
+        state = {"left": len(futs), "ok": True}
+
+        def done(f):
+            with self.lock:
+                state["left"] -= 1
+                if f.exception() is not None:
+                    state["ok"] = False
+                last = state["left"] == 0 and state["ok"]
+            if last:
+                try:
+                    fn(*a)
+                except BaseException as e:   # reported by drain
+                    with self.lock:
+                        self.errors.append(e)
+
+        for f in futs:
+            f.add_done_callback(done)
 
     def drain(self):
         futs, self.futs = self.futs, []
         for f in futs:
             f.result()
+        with self.lock:
+            errs, self.errors = self.errors, []
+        if errs:
+            raise errs[0]
 
     def close(self):
-        try:
-            self.drain()
-        finally:
-            if self.pool is not None:
-                self.pool.shutdown()
+        # workers first: a when_all callback runs in the worker that finished the last write
+        if self.pool is not None:
+            self.pool.shutdown(wait=True)
+        self.drain()
 
 
 def run_sequence(ds, seq, results, device=-1, extra=(), writer=None):
@@ -257,7 +290,7 @@ def run_sequence(ds, seq, results, device=-1, extra=(), writer=None):
     f0, f1 = ds.frame(seq, 0), ds.frame(seq, 1)
     a, w, h = open_gray(f0)
     b, w, h = open_gray(f1)
-    writer.submit(save_gray, frame_diff(a, b), w, h, os.path.join(out, "diff.png"))
+    seq_futs = [writer.submit(save_gray, frame_diff(a, b), w, h, os.path.join(out, "diff.png"))]
     done = []
     gt = ds.gt_flow(seq)
     for algo, algo_args in ALGOS:
@@ -270,9 +303,10 @@ def run_sequence(ds, seq, results, device=-1, extra=(), writer=None):
                 f"--device={device}", *extra]
         if gt:
             argv.append(f"--ground-truth={gt}")
+        n0 = len(writer.futs)
         u, v, _ = run_main(argv, p("log"), writer)
-        writer.submit(color_flow_arrays, u, v, w, h, p("png"))
-        writer.submit(touch, marker)
+        files = writer.futs[n0:] + [writer.submit(color_flow_arrays, u, v, w, h, p("png"))]
+        writer.when_all(files + seq_futs, touch, marker)   # the marker only after its files
         done.append(algo)
     if own:
         writer.close()
@@ -307,7 +341,7 @@ def worker(args, rank, world, device):
     import time
     t0, t0_wall = time.perf_counter(), time.time()
     mine = shard(jobs(args), rank, world)
-    writer = Writer(threads=1)
+    writer = Writer(threads=4)
     try:
         for ds, seq in mine:
             done = run_sequence(ds, seq, args.results, device, args.extra, writer)

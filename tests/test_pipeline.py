@@ -96,19 +96,32 @@ def test_color_from_arrays_matches_flo_round_trip(tmp_path):
     assert np.array_equal(np.asarray(Image.open(tmp_path / "a.png")), np.asarray(Image.open(tmp_path / "b.png")))
 
 
-def test_writer_order_and_errors(tmp_path):
-    w = pipeline.Writer(threads=1)
-    seen = []
-    for i in range(20):
-        w.submit(seen.append, i)
+def test_writer_markers_after_files_and_errors(tmp_path):
+    import threading
+    import time
+    w = pipeline.Writer(threads=4)
+    seen, lock = [], threading.Lock()
+
+    def slow(i):
+        time.sleep(0.01 * (i % 3))
+        with lock:
+            seen.append(i)
+    for g in range(5):
+        futs = [w.submit(slow, 10 * g + i) for i in range(4)]
+        w.when_all(futs, lambda g=g: seen.append(("marker", g)))
     w.drain()
-    assert seen == list(range(20))
+    time.sleep(0.05)   # callbacks run in the worker that finished last
+    for g in range(5):
+        k = seen.index(("marker", g))
+        assert all(seen.index(10 * g + i) < k for i in range(4))
 
     def boom():
         raise OSError("disk full")
-    w.submit(boom)
+    f = w.submit(boom)
+    w.when_all([f], lambda: seen.append("never"))
     with pytest.raises(OSError):
         w.close()
+    assert "never" not in seen
 
 
 def test_run_loop_markers_and_restart(tmp_path, monkeypatch):
