@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Outer iterations/s of the Benamou-Brenier solve on one GPU at the SURVEY.md §8 config sizes
 (synthetic translating-Gaussian pairs; r = 1, eps = 1e-2, stop rules off).
-usage: python tools/size_sweep.py [NxxNyxNt ...]"""
+usage: python tools/size_sweep.py [NxxNyxNt ...] [--mode=M] [--kernels]"""
 import sys
 import time
 
@@ -12,14 +12,15 @@ from foto.synthetic import translating_gaussian  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 kern = "--kernels" in sys.argv   # also a timed pass with HIP events around every launch
+mode = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--mode=")), "3"))
 sizes = args or ["64x64x8", "584x388x32", "640x480x32", "1024x1024x64"]
 for sz in sizes:
     Nx, Ny, Nt = (int(v) for v in sz.split("x"))
     rho0, rhoT = translating_gaussian(Nx, Ny)
-    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, device=0, cg_mode=2) as s:
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, device=0, cg_mode=mode) as s:
         s.iterate(2, 0.0, stop_rules=False)
         s.sync()
-        k = 5
+        k = 10
         t = time.perf_counter()
         s.iterate(k, 0.0, stop_rules=False)
         s.sync()
