@@ -858,6 +858,174 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, co
     }
 }
 
+// The small levels in one block (FOTO_MG_TAIL=1; off by default -- measured slower): below ~80x60
+// cells a level kernel is a few blocks whose launch and drain look costlier than its work (6-9 us
+// each, five of the 13 launches of a PCG iteration at 640x480).  k_mg_tail runs the down legs of
+// levels l0 .. c-1, the coarsest solve and the up legs back to l0 in one 1024-thread block, level
+// arrays in global memory (L2-resident), a barrier between stages, every cell with the level
+// kernels' formulas in their order (the same preconditioner bit for bit).  Replayed from the
+// hipGraph the separate launches are cheap, and one CU's stages are latency-bound: 180 us per
+// PCG iteration with the tail from 80x60 down, 137.6 from 40x30, 133.5-133.8 without (r03, A/B on
+// one box).
+constexpr int MG_TAIL_MAX = 6;
+constexpr int MG_TAIL_CELLS = 1300;   // levels at most this many cells join the tail (5000: slower)
+struct MGTail {
+    int nl;                            // levels in the tail; the last one is the coarsest
+    MGLev L[MG_TAIL_MAX];
+    double* f[MG_TAIL_MAX];
+    double* x[MG_TAIL_MAX];
+    double* y[MG_TAIL_MAX];
+};
+
+__global__ __launch_bounds__(1024) void k_mg_tail(MGTail T, const CGScal* S) {
+    if (S->done) return;
+    const int tid = threadIdx.x;
+    const int nl = T.nl;
+    for (int l = 0; l + 1 < nl; ++l) {   // down legs (k_mg_down2's three stages, level-wide)
+        const MGLev L = T.L[l];
+        const int w = L.w, h = L.h;
+        const int64_t n = (int64_t)w * h;
+        const double* f = T.f[l];
+        double* x = T.x[l];
+        double* rr = T.y[l];   // the residual; y is the up leg's output, free until then
+        for (int64_t i = tid; i < n; i += 1024) {
+            double z0, z1, z2;
+            mg_dinv(L, i, f[i], f[n + i], f[2 * n + i], z0, z1, z2);
+            x[i] = z0 * MG_OMEGA; x[n + i] = z1 * MG_OMEGA; x[2 * n + i] = z2 * MG_OMEGA;
+        }
+        __syncthreads();
+        for (int64_t i = tid; i < n; i += 1024) {
+            const int gy = (int)(i / w), gx = (int)(i - (int64_t)gy * w);
+            double a0, a1, a2, v0, v1, v2;
+            mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return x[fl * n + i + (int64_t)dy * w + dx]; }, a0,
+                       a1, a2, v0, v1, v2);
+            rr[i] = f[i] - a0; rr[n + i] = f[n + i] - a1; rr[2 * n + i] = f[2 * n + i] - a2;
+        }
+        __syncthreads();
+        const int wc = T.L[l + 1].w, hc = T.L[l + 1].h;
+        const int64_t nc = (int64_t)wc * hc;
+        double* fc = T.f[l + 1];
+        for (int64_t I0 = tid; I0 < nc; I0 += 1024) {
+            const int J = (int)(I0 / wc), K = (int)(I0 - (int64_t)J * wc);
+            double wy[4], wx[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int y = 2 * J - 1 + d, xx = 2 * K - 1 + d;
+                wy[d] = (y >= 0 && y < h) ? mg_w1(y, J, hc) : 0.0;
+                wx[d] = (xx >= 0 && xx < w) ? mg_w1(xx, K, wc) : 0.0;
+            }
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < 4; ++dy) {
+                double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+                const int y = 2 * J - 1 + dy;
+#pragma unroll
+                for (int dx = 0; dx < 4; ++dx) {
+                    const int xx = 2 * K - 1 + dx;
+                    const bool in = y >= 0 && y < h && xx >= 0 && xx < w;
+                    const int64_t i = in ? (int64_t)y * w + xx : 0;
+                    b0 += wx[dx] * (in ? rr[i] : 0.0);
+                    b1 += wx[dx] * (in ? rr[n + i] : 0.0);
+                    b2 += wx[dx] * (in ? rr[2 * n + i] : 0.0);
+                }
+                a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * b2;
+            }
+            fc[I0] = 0.25 * a0;
+            fc[nc + I0] = 0.25 * a1;
+            fc[2 * nc + I0] = 0.25 * a2;
+        }
+        __syncthreads();
+    }
+    {   // the coarsest level: k_mg_coarse<false>'s sweeps
+        const MGLev L = T.L[nl - 1];
+        __shared__ double xs[2][3 * MG_COARSE];
+        const int n = L.w * L.h, i = tid;
+        const bool in = i < n;
+        const int y = in ? i / L.w : 0, xx = in ? i - y * L.w : 0;
+        const double* f = T.f[nl - 1];
+        double f0 = 0, f1 = 0, f2v = 0;
+        double b[6] = {0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
+        const bool hxm = xx > 0, hxp = xx < L.w - 1, hym = y > 0, hyp = y < L.h - 1;
+        const double c = (double)mg_ncount(xx, y, L.w, L.h);
+        if (in) {
+            f0 = f[i]; f1 = f[n + i]; f2v = f[2 * n + i];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) { b[k] = L.B[k * n + i]; d[k] = L.Dinv[k * n + i]; }
+            const double z0 = d[0] * f0 + d[1] * f1 + d[2] * f2v, z1 = d[1] * f0 + d[3] * f1 + d[4] * f2v,
+                         z2 = d[2] * f0 + d[4] * f1 + d[5] * f2v;
+            xs[0][i] = MG_OMEGA * z0; xs[0][n + i] = MG_OMEGA * z1; xs[0][2 * n + i] = MG_OMEGA * z2;
+        }
+        __syncthreads();
+        const double sc[3] = {L.s0, L.s1, L.s2};
+        int cur = 0;
+        for (int sweep = 1; sweep < MG_CSWEEPS; ++sweep) {
+            if (in) {
+                const double* xc = xs[cur];
+                double v[3], a[3];
+#pragma unroll
+                for (int fl = 0; fl < 3; ++fl) {
+                    const double* q = xc + fl * n;
+                    v[fl] = q[i];
+                    const double nb = (hxm ? q[i - 1] : 0.0) + (hxp ? q[i + 1] : 0.0) + (hym ? q[i - L.w] : 0.0) +
+                                      (hyp ? q[i + L.w] : 0.0);
+                    a[fl] = sc[fl] * (c * v[fl] - nb);
+                }
+                const double r0 = f0 - (a[0] + b[0] * v[0] + b[1] * v[1] + b[2] * v[2]);
+                const double r1 = f1 - (a[1] + b[1] * v[0] + b[3] * v[1] + b[4] * v[2]);
+                const double r2 = f2v - (a[2] + b[2] * v[0] + b[4] * v[1] + b[5] * v[2]);
+                xs[cur ^ 1][i] = v[0] + MG_OMEGA * (d[0] * r0 + d[1] * r1 + d[2] * r2);
+                xs[cur ^ 1][n + i] = v[1] + MG_OMEGA * (d[1] * r0 + d[3] * r1 + d[4] * r2);
+                xs[cur ^ 1][2 * n + i] = v[2] + MG_OMEGA * (d[2] * r0 + d[4] * r1 + d[5] * r2);
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+        if (in) {
+            double* xo = T.x[nl - 1];
+            xo[i] = xs[cur][i]; xo[n + i] = xs[cur][n + i]; xo[2 * n + i] = xs[cur][2 * n + i];
+        }
+        __syncthreads();
+    }
+    for (int l = nl - 2; l >= 0; --l) {   // up legs (k_mg_up2<false>'s two stages, level-wide)
+        const MGLev L = T.L[l];
+        const int w = L.w, h = L.h;
+        const int64_t n = (int64_t)w * h;
+        const int wc = T.L[l + 1].w, hc = T.L[l + 1].h;
+        const int64_t nc = (int64_t)wc * hc;
+        const double* ec = (l + 1 == nl - 1) ? T.x[nl - 1] : T.y[l + 1];
+        double* x = T.x[l];   // x' = x + P ec, in place
+        for (int64_t i = tid; i < n; i += 1024) {
+            const int gy = (int)(i / w), gx = (int)(i - (int64_t)gy * w);
+            const int X0 = gx >> 1, Y0 = gy >> 1;
+            int X1 = (gx & 1) ? X0 + 1 : X0 - 1, Y1 = (gy & 1) ? Y0 + 1 : Y0 - 1;
+            X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
+            Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
+            const int64_t c00 = (int64_t)Y0 * wc + X0, c01 = (int64_t)Y0 * wc + X1, c10 = (int64_t)Y1 * wc + X0,
+                          c11 = (int64_t)Y1 * wc + X1;
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) {
+                const double* e = ec + fl * nc;
+                x[fl * n + i] = x[fl * n + i] + (0.5625 * e[c00] + 0.1875 * e[c01] + 0.1875 * e[c10] + 0.0625 * e[c11]);
+            }
+        }
+        __syncthreads();
+        const double* f = T.f[l];
+        double* out = T.y[l];
+        for (int64_t i = tid; i < n; i += 1024) {
+            const int gy = (int)(i / w), gx = (int)(i - (int64_t)gy * w);
+            double a0, a1, a2, v0, v1, v2, z0, z1, z2;
+            mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return x[fl * n + i + (int64_t)dy * w + dx]; }, a0,
+                       a1, a2, v0, v1, v2);
+            const double f0 = f[i], f1 = f[n + i], f2v = f[2 * n + i];
+            mg_dinv(L, i, f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
+            out[i] = v0 + MG_OMEGA * z0;
+            out[n + i] = v1 + MG_OMEGA * z1;
+            out[2 * n + i] = v2 + MG_OMEGA * z2;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace foto
 
 // ============================================================================ GN plan (host)
@@ -889,6 +1057,7 @@ struct foto_gn_plan {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     int last_its = 0;
     double last[4] = {0, 0, 0, 0};   // ms setup+upload, ms PCG, iterations, iterations launched
+    bool tail = false;               // small levels in one block (k_mg_tail, FOTO_MG_TAIL=1; measured slower)
 
     MGLev desc(size_t l) const {
         const Lev& L = lev[l];
@@ -924,18 +1093,42 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
         FOTO_HIP_CHECK(hipGetLastError());
         return 0;
     }
-    for (size_t l = 0; l + 1 < nl; ++l) {
+    // the tail: the first level l0 >= 1 from which every level has at most MG_TAIL_CELLS cells
+    size_t l0 = nl;
+    if (P->tail) {
+        for (size_t l = 1; l < nl; ++l)
+            if ((int64_t)P->lev[l].w * P->lev[l].h <= MG_TAIL_CELLS && nl - l <= (size_t)MG_TAIL_MAX) { l0 = l; break; }
+    }
+    const size_t ldown = std::min(l0, nl - 1);
+    for (size_t l = 0; l < ldown; ++l) {
         const auto& L = P->lev[l];
         const auto& C = P->lev[l + 1];
         k_mg_down2<<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x, C.f);
         FOTO_HIP_CHECK(hipGetLastError());
     }
     const size_t c = nl - 1;
-    k_mg_coarse<false><<<1, mg_coarse_threads(P->lev[c]), 0, s>>>(P->desc(c), P->dS, P->lev[c].f, P->lev[c].x,
-                                                                  nullptr);
-    FOTO_HIP_CHECK(hipGetLastError());
-    const double* e = P->lev[c].x;
-    for (size_t l = nl - 1; l-- > 0;) {
+    const double* e = nullptr;
+    size_t lup = nl - 1;   // up legs below this level run as level kernels
+    if (l0 < nl) {
+        MGTail T{};
+        T.nl = (int)(nl - l0);
+        for (size_t l = l0; l < nl; ++l) {
+            T.L[l - l0] = P->desc(l);
+            T.f[l - l0] = P->lev[l].f;
+            T.x[l - l0] = P->lev[l].x;
+            T.y[l - l0] = P->lev[l].y;
+        }
+        k_mg_tail<<<1, 1024, 0, s>>>(T, P->dS);
+        FOTO_HIP_CHECK(hipGetLastError());
+        e = (l0 == c) ? P->lev[c].x : P->lev[l0].y;
+        lup = l0;
+    } else {
+        k_mg_coarse<false><<<1, mg_coarse_threads(P->lev[c]), 0, s>>>(P->desc(c), P->dS, P->lev[c].f, P->lev[c].x,
+                                                                      nullptr);
+        FOTO_HIP_CHECK(hipGetLastError());
+        e = P->lev[c].x;
+    }
+    for (size_t l = lup; l-- > 0;) {
         const auto& L = P->lev[l];
         const auto& C = P->lev[l + 1];
         if (l == 0) {
@@ -990,6 +1183,10 @@ static int gn_plan_init(foto_gn_plan* P) {
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
     tr.mark("pinned scalars");   // (the pinned staging is made during the first solve: gn_staging)
     P->nb_pix = flat_blocks((int64_t)n);
+    {
+        const char* e = getenv("FOTO_MG_TAIL");
+        P->tail = e && atoi(e) != 0;
+    }
     // level geometry
     int lw = w, lh = h;
     double sc = 1.0;
