@@ -2779,6 +2779,15 @@ struct SpecImpl {
     double* gq_part = nullptr;    // gq_nblk histograms
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
     double* gq_tab = nullptr;
+    GqBins* gq_bins = nullptr;    // bin edges of the measure and the solution table
+    // bin-ordered histogram (k_gq_hist_perm): the box's voxels grouped by bin, chunked
+    bool gq_perm = false;
+    unsigned* gq_permv = nullptr;
+    GqChunk* gq_chunks = nullptr;
+    int gq_nch = 0;
+    int* gq_cfirst = nullptr;     // [GQ_NB + 1] first chunk of each bin
+    double* gq_rowmu = nullptr;   // mu_t + mu_y per box row
+    double* gq_ppart = nullptr;   // [gq_nch][GQ_NM] chunk sums
 
     // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
     // sharded always); the pass a plan finishes marks the solve done in its tail
@@ -2841,6 +2850,8 @@ static int cus_count() {   // CUs of the current device (cached per device ordin
     if (dev >= 0 && dev < 64) cache[dev] = cus;
     return cus;
 }
+
+static int gq_build_perm(SpecImpl* P, hipStream_t s);
 
 int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, int sstep, hipStream_t s) {
     // cg_mode 3: the Gauss-compressed CG, with the s-step machinery kept for the (rare) redo
@@ -2995,8 +3006,75 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;   // + the first reduction level
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * (P->gq_nblk + ngroups), &b)); P->gq_part = (double*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
-        FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
+        FOTO_TRY(P->alloc(2 * GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
+        FOTO_TRY(P->alloc(sizeof(GqBins), &b)); P->gq_bins = (GqBins*)b;
+        k_gq_bins<<<1, 256, 0, s>>>(P->gq_bins);
+        FOTO_HIP_CHECK(hipGetLastError());
+        const char* ep = getenv("FOTO_GQ_PERM");   // 0: the row-scan LDS histogram (A/B runs)
+        P->gq_perm = gq_perm_ok(g.Nx, rows) && !(ep && atoi(ep) == 0);
+        if (P->gq_perm) FOTO_TRY(gq_build_perm(P, s));
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+// the bin-ordered voxel list of the box (k_gq_hist_perm): per-row run counts by bin, a scan over
+// the rows of each bin, the bins' first entries on the host (it also cuts the chunks), then
+// every row writes its runs.  Once per plan; the count table is scratch.
+static int gq_build_perm(SpecImpl* P, hipStream_t s) {
+    const SpecTab T = P->tab();
+    const int rows = P->g.Nt * P->nyl;
+    const int64_t N = (int64_t)rows * P->g.Nx;
+    void* b = nullptr;
+    FOTO_TRY(P->alloc(sizeof(double) * rows, &b)); P->gq_rowmu = (double*)b;
+    k_gq_rowmu<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_rowmu);
+    FOTO_HIP_CHECK(hipGetLastError());
+    int* cnt = nullptr;
+    const size_t ncnt = (size_t)GQ_NB * rows;
+    FOTO_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int) * (ncnt + 2 * GQ_NB + 1)));
+    int* tot = cnt + ncnt;
+    int* first = tot + GQ_NB;
+    int rc = 0;
+    std::vector<int> htot(GQ_NB), hfirst(GQ_NB + 1), cfirst(GQ_NB + 1);
+    std::vector<GqChunk> ch;
+    do {
+        if (hipMemsetAsync(cnt, 0, sizeof(int) * ncnt, s) != hipSuccess) { rc = -1; break; }
+        k_gq_perm_count<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, P->gq_rowmu, P->c0, 1.0 / P->c1, cnt);
+        k_gq_perm_scan<<<GQ_NB, 256, 0, s>>>(rows, cnt, tot);
+        if (hipMemcpyAsync(htot.data(), tot, sizeof(int) * GQ_NB, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
+        int64_t acc = 0;
+        for (int bb = 0; bb < GQ_NB; ++bb) {
+            hfirst[bb] = (int)acc;
+            cfirst[bb] = (int)ch.size();
+            for (int st = 0; st < htot[bb]; st += GQ_PCH) ch.push_back(GqChunk{bb, (int)acc + st, std::min(GQ_PCH, htot[bb] - st), 0});
+            acc += htot[bb];
+        }
+        hfirst[GQ_NB] = (int)acc;
+        cfirst[GQ_NB] = (int)ch.size();
+        if (acc != N) { set_error("gauss perm: %lld voxels binned, box has %lld", (long long)acc, (long long)N); rc = -1; break; }
+        P->gq_nch = (int)ch.size();
+        if (P->alloc(sizeof(unsigned) * N, &b)) { rc = -1; break; }
+        P->gq_permv = (unsigned*)b;
+        if (P->alloc(sizeof(GqChunk) * ch.size(), &b)) { rc = -1; break; }
+        P->gq_chunks = (GqChunk*)b;
+        if (P->alloc(sizeof(int) * (GQ_NB + 1), &b)) { rc = -1; break; }
+        P->gq_cfirst = (int*)b;
+        if (P->alloc(sizeof(double) * GQ_NM * ch.size(), &b)) { rc = -1; break; }
+        P->gq_ppart = (double*)b;
+        if (hipMemcpyAsync(first, hfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(P->gq_chunks, ch.data(), sizeof(GqChunk) * ch.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(P->gq_cfirst, cfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = -1; break;
+        }
+        k_gq_perm_fill<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, P->gq_rowmu, P->c0, 1.0 / P->c1, cnt, first,
+                                                          P->gq_permv);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
+    } while (false);
+    (void)hipFree(cnt);
+    if (rc) {
+        set_error("gauss perm build failed");
+        return -1;
     }
     return 0;
 }
@@ -3141,9 +3219,22 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
 // 1024-thread block per CU (the 64 KB table allows one)
 static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
     const SpecTab T = P->tab();
+    // FOTO_GQ_XPERM=1: x^ in bin order (k_gq_xhat_perm, coefficients in SGPRs) -- measured
+    // slower than the row-wise LDS-table kernel (66 vs 58 us at 640x480x32: the bin-order
+    // stores land as scattered 8-B writes), kept for A/B runs
+    static const bool xperm = [] {
+        const char* e = getenv("FOTO_GQ_XPERM");
+        return e && atoi(e) == 1;
+    }();
+    if (P->gq_perm && xperm) {
+        const int nbk = std::max(1, (P->gq_nch + 3) / 4);
+        k_gq_xhat_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_tab, P->gq, P->gq_bins,
+                                           P->gq_rowmu, P->c0, 1.0 / P->c1, out);
+        return hipGetLastError();
+    }
     const int rows = P->g.Nt * P->nyl;
     const int nb = std::max(1, std::min(cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
-    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->c0, 1.0 / P->c1, out);
+    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins, P->c0, 1.0 / P->c1, out);
     return hipGetLastError();
 }
 
@@ -3202,7 +3293,17 @@ static int tcol_inverse(SpecImpl* P, double* b, double* x, double rtol, int maxi
 static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     const SpecTab T = P->tab();
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_gq_hist<<<P->gq_nblk, GQ_HNTH, 0, s>>>(T, P->bh, P->c0, 1.0 / P->c1, P->gq_part);
+    if (P->gq_perm) {
+        const int nbk = std::max(1, (P->gq_nch + 3) / 4);
+        k_gq_hist_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_bins, P->gq_rowmu,
+                                           P->c0, 1.0 / P->c1, P->gq_ppart);
+        FOTO_HIP_CHECK(hipGetLastError());
+        k_gq_perm_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
+        FOTO_HIP_CHECK(hipGetLastError());
+        if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
+        return 0;
+    }
+    k_gq_hist<<<P->gq_nblk, GQ_HNTH, 0, s>>>(T, P->bh, P->gq_bins, P->c0, 1.0 / P->c1, P->gq_part);
     FOTO_HIP_CHECK(hipGetLastError());
     const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;
     double* grp = P->gq_part + (size_t)P->gq_nblk * GQ_HIST;
@@ -3217,11 +3318,11 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
 // the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
 static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->world, P->c0, P->c1, P->gqn);
+    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->world, P->c0, P->c1, P->gqn);
     FOTO_HIP_CHECK(hipGetLastError());
     k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, P->gq);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->c0, P->c1, P->gq_tab);
+    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->c0, P->c1, P->gq_tab);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
     FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq, P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
