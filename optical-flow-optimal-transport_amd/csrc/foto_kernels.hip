@@ -530,6 +530,30 @@ __device__ __noinline__ double proj_trig_z(double al, double rho) {
     return 1.632993161855452 * sm * cos(0.3333333333333333 * acos(1.8371173070873836 * rho / (m * sm)));
 }
 
+// S^(1/3) and S^(-1/3) for finite S > 0 without the library cbrt and a division: S = m 2^e
+// (m in [0.5, 1)), e = 3q + s (s in {0, 1, 2}), S' = m 2^s in [0.5, 4); y ~ S'^(-1/3) from the
+// fp32 log2 / exp2 (~1e-7 relative), two Newton steps y <- y (4 - S' y^3) / 3 (quadratic:
+// rounding level), then S^(1/3) = S' y^2 2^q and S^(-1/3) = y 2^-q.  Within 2-3 ulp of the
+// rounded values (the reference's x ** (1/3) is itself within an ulp of them).
+#ifndef FOTO_PROJ_FAST
+#define FOTO_PROJ_FAST 1
+#endif
+__device__ __forceinline__ void cbrt_pair(double S, double& c, double& ic) {
+    const int e = __builtin_amdgcn_frexp_exp(S);
+    const double m = __builtin_amdgcn_frexp_mant(S);
+    const int q = (e >= 0) ? e / 3 : -((2 - e) / 3);   // floor(e / 3)
+    const double Sp = __builtin_amdgcn_ldexp(m, e - 3 * q);
+    const float yf = __builtin_amdgcn_exp2f(-0.3333333333f * __builtin_amdgcn_logf((float)Sp));
+    double y = (double)yf;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double y3 = (y * y) * y;
+        y = (y * fma(-Sp, y3, 4.0)) * 0.3333333333333333;
+    }
+    c = __builtin_amdgcn_ldexp((Sp * y) * y, q);
+    ic = __builtin_amdgcn_ldexp(y, -q);
+}
+
 __device__ __forceinline__ void project_K(double al, double b1, double b2, double& oa, double& o1, double& o2) {
     if (2.0 * al + b1 * b1 + b2 * b2 <= 0.0) {
         oa = al; o1 = b1; o2 = b2;
@@ -543,8 +567,19 @@ __device__ __forceinline__ void project_K(double al, double b1, double b2, doubl
         const double S = 0.3535533905932738 * rho +
                          0.16666666666666666 * sqrt(1.3333333333333333 * (al * al * al) + 4.0 * (al * al) +
                                                     4.5 * (rho * rho) + 4.0 * al + 1.3333333333333333);
+#if FOTO_PROJ_FAST
+        double c, ic;
+        if (S > 0.0 && S <= 1.7976931348623157e308) {
+            cbrt_pair(S, c, ic);
+        } else {
+            c = cbrt(S);
+            ic = 1.0 / c;
+        }
+        const double zh = fma(-0.3333333333333333 * ap1, ic, c);
+#else
         const double c = cbrt(S);
         const double zh = (-0.3333333333333333 * ap1) / c + c;
+#endif
         aH = -(zh * zh);
         rH = SQRT2 * zh;
     } else {
@@ -554,8 +589,14 @@ __device__ __forceinline__ void project_K(double al, double b1, double b2, doubl
     }
     oa = aH;
     if (rho > 0.0) {
+#if FOTO_PROJ_FAST
+        const double ir = 1.0 / rho;
+        o1 = rH * (b1 * ir);
+        o2 = rH * (b2 * ir);
+#else
         o1 = rH * (b1 / rho);
         o2 = rH * (b2 / rho);
+#endif
     } else {   // atan2(+-0, +0) = +-0, atan2(+-0, -0) = +-pi
         o1 = signbit(b1) ? -rH : rH;
         o2 = 0.0;

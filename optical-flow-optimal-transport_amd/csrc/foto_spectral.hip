@@ -2772,22 +2772,20 @@ struct SpecImpl {
     double c0 = 0, c1 = 1;
     // Gauss-compressed CG (cg_mode 3, foto_gauss.inc); gauss_active: the solve in flight uses it
     bool gauss = false, gauss_active = false;
-    int gq_nblk = 0;
     GqState* gq = nullptr;
     GqState* hgq = nullptr;       // pinned: the header (K, status, conv, done, bn2, rn2)
     GqNodes* gqn = nullptr;
-    double* gq_part = nullptr;    // gq_nblk histograms
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
     double* gq_tab = nullptr;
     GqBins* gq_bins = nullptr;    // bin edges of the measure and the solution table
     // bin-ordered histogram (k_gq_hist_perm): the box's voxels grouped by bin, chunked
-    bool gq_perm = false;
     unsigned* gq_permv = nullptr;
     GqChunk* gq_chunks = nullptr;
     int gq_nch = 0;
     int* gq_cfirst = nullptr;     // [GQ_NB + 1] first chunk of each bin
     double* gq_rowmu = nullptr;   // mu_t + mu_y per box row
     double* gq_ppart = nullptr;   // [gq_nch][GQ_NM] chunk sums
+    GqExact* gq_exact = nullptr;  // exact bins (the whole grid's distinct eigenvalues)
 
     // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
     // sharded always); the pass a plan finishes marks the solve done in its tail
@@ -2995,88 +2993,137 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     FOTO_TRY(P->alloc(sizeof(SStep), &b)); P->S2 = (SStep*)b;
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS2, sizeof(SStep)));
     FOTO_TRY(reset_s2(P, s));   // c0, c1 for the fused INIT (solve_tcol)
-    P->gauss = gauss;
-    if (gauss) {
-        // histogram blocks: one per CU (each holds 4 private 32 KB histograms), at most one per 4 rows
-        P->gq_nblk = std::max(1, std::min(cus_count(), (rows + 3) / 4));
+    // the Gauss-compressed CG needs the bin-ordered voxel list; boxes its packing does not
+    // cover run the s-step CG (decided on the whole grid, so every rank agrees)
+    P->gauss = gauss && gq_perm_ok(g.Nx, g.Nt * g.Ny);
+    if (P->gauss) {
         FOTO_TRY(P->alloc(sizeof(GqState), &b)); P->gq = (GqState*)b;
         FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
         FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq, sizeof(GqState)));
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
-        const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;   // + the first reduction level
-        FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * (P->gq_nblk + ngroups), &b)); P->gq_part = (double*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
         FOTO_TRY(P->alloc(2 * GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
         FOTO_TRY(P->alloc(sizeof(GqBins), &b)); P->gq_bins = (GqBins*)b;
         k_gq_bins<<<1, 256, 0, s>>>(P->gq_bins);
         FOTO_HIP_CHECK(hipGetLastError());
-        const char* ep = getenv("FOTO_GQ_PERM");   // 0: the row-scan LDS histogram (A/B runs)
-        P->gq_perm = gq_perm_ok(g.Nx, rows) && !(ep && atoi(ep) == 0);
-        if (P->gq_perm) FOTO_TRY(gq_build_perm(P, s));
+        FOTO_TRY(P->alloc(sizeof(GqExact), &b)); P->gq_exact = (GqExact*)b;
+        FOTO_TRY(gq_build_perm(P, s));
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
     }
     return 0;
 }
 
-// the bin-ordered voxel list of the box (k_gq_hist_perm): per-row run counts by bin, a scan over
-// the rows of each bin, the bins' first entries on the host (it also cuts the chunks), then
-// every row writes its runs.  Once per plan; the count table is scratch.
-static int gq_build_perm(SpecImpl* P, hipStream_t s) {
-    const SpecTab T = P->tab();
-    const int rows = P->g.Nt * P->nyl;
-    const int64_t N = (int64_t)rows * P->g.Nx;
-    void* b = nullptr;
-    FOTO_TRY(P->alloc(sizeof(double) * rows, &b)); P->gq_rowmu = (double*)b;
-    k_gq_rowmu<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_rowmu);
+// The bin-ordered voxel list of a box T (k_gq_hist_perm): per-row run counts by bin, a scan
+// over the rows of each bin, the bins' first entries (host and device), then every row writes
+// its runs.  perm (rows * Nx), rowmu (rows), first_d / tot_d (GQ_NB + 1 / GQ_NB) are the
+// caller's; the count table is scratch.
+static int gq_perm_lists(SpecImpl* P, const SpecTab& T, unsigned* perm, double* rowmu, int* first_d, int* tot_d,
+                         std::vector<int>& htot, std::vector<int>& hfirst, hipStream_t s) {
+    const int rows = T.Nt * T.nyl;
+    const int64_t N = (int64_t)rows * T.Nx;
+    k_gq_rowmu<<<(rows + 255) / 256, 256, 0, s>>>(T, rowmu);
     FOTO_HIP_CHECK(hipGetLastError());
     int* cnt = nullptr;
     const size_t ncnt = (size_t)GQ_NB * rows;
-    FOTO_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int) * (ncnt + 2 * GQ_NB + 1)));
-    int* tot = cnt + ncnt;
-    int* first = tot + GQ_NB;
+    FOTO_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int) * ncnt));
     int rc = 0;
-    std::vector<int> htot(GQ_NB), hfirst(GQ_NB + 1), cfirst(GQ_NB + 1);
-    std::vector<GqChunk> ch;
+    htot.assign(GQ_NB, 0);
+    hfirst.assign(GQ_NB + 1, 0);
     do {
         if (hipMemsetAsync(cnt, 0, sizeof(int) * ncnt, s) != hipSuccess) { rc = -1; break; }
-        k_gq_perm_count<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, P->gq_rowmu, P->c0, 1.0 / P->c1, cnt);
-        k_gq_perm_scan<<<GQ_NB, 256, 0, s>>>(rows, cnt, tot);
-        if (hipMemcpyAsync(htot.data(), tot, sizeof(int) * GQ_NB, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        k_gq_perm_count<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, rowmu, 1.0 / P->c1, cnt);
+        k_gq_perm_scan<<<GQ_NB, 256, 0, s>>>(rows, cnt, tot_d);
+        if (hipMemcpyAsync(htot.data(), tot_d, sizeof(int) * GQ_NB, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
         int64_t acc = 0;
         for (int bb = 0; bb < GQ_NB; ++bb) {
             hfirst[bb] = (int)acc;
-            cfirst[bb] = (int)ch.size();
-            for (int st = 0; st < htot[bb]; st += GQ_PCH) ch.push_back(GqChunk{bb, (int)acc + st, std::min(GQ_PCH, htot[bb] - st), 0});
             acc += htot[bb];
         }
         hfirst[GQ_NB] = (int)acc;
-        cfirst[GQ_NB] = (int)ch.size();
-        if (acc != N) { set_error("gauss perm: %lld voxels binned, box has %lld", (long long)acc, (long long)N); rc = -1; break; }
-        P->gq_nch = (int)ch.size();
-        if (P->alloc(sizeof(unsigned) * N, &b)) { rc = -1; break; }
-        P->gq_permv = (unsigned*)b;
-        if (P->alloc(sizeof(GqChunk) * ch.size(), &b)) { rc = -1; break; }
-        P->gq_chunks = (GqChunk*)b;
-        if (P->alloc(sizeof(int) * (GQ_NB + 1), &b)) { rc = -1; break; }
-        P->gq_cfirst = (int*)b;
-        if (P->alloc(sizeof(double) * GQ_NM * ch.size(), &b)) { rc = -1; break; }
-        P->gq_ppart = (double*)b;
-        if (hipMemcpyAsync(first, hfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(P->gq_chunks, ch.data(), sizeof(GqChunk) * ch.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(P->gq_cfirst, cfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s) != hipSuccess) {
-            rc = -1; break;
+        if (acc != N) {
+            set_error("gauss perm: %lld voxels binned, box has %lld", (long long)acc, (long long)N);
+            rc = -1;
+            break;
         }
-        k_gq_perm_fill<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, P->gq_rowmu, P->c0, 1.0 / P->c1, cnt, first,
-                                                          P->gq_permv);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
+        if (hipMemcpyAsync(first_d, hfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        k_gq_perm_fill<<<(rows + 255) / 256, 256, 0, s>>>(T, P->gq_bins, rowmu, 1.0 / P->c1, cnt, first_d, perm);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) rc = -1;
     } while (false);
     (void)hipFree(cnt);
-    if (rc) {
-        set_error("gauss perm build failed");
-        return -1;
+    if (rc) set_error("gauss perm build failed");
+    return rc ? -1 : 0;
+}
+
+// this box's list and chunks, and the exact bins of the whole grid (from the box's list when the
+// box is the grid, else from a scratch list of the grid: every rank derives the same table)
+static int gq_build_perm(SpecImpl* P, hipStream_t s) {
+    const SpecTab T = P->tab();
+    // exact bins of at most GQ_M points (their points are the rule).  FOTO_GQ_EXACT (A/B): -1
+    // none; up to GQ_XS = 16 also takes bins of 9-16 points through the Stieltjes procedure --
+    // measured less accurate (the 5-step iterate of an 8x24x20 grid 1.6e-10 from scipy's against
+    // 2.3e-12; the node / weight solve loses digits on clustered points), not the default
+    const char* ex = getenv("FOTO_GQ_EXACT");
+    const int xmax = ex ? std::min(atoi(ex), GQ_XS) : GQ_M;
+    const int rows = P->g.Nt * P->nyl;
+    const int64_t N = (int64_t)rows * P->g.Nx;
+    void* b = nullptr;
+    FOTO_TRY(P->alloc(sizeof(double) * rows, &b)); P->gq_rowmu = (double*)b;
+    FOTO_TRY(P->alloc(sizeof(unsigned) * N, &b)); P->gq_permv = (unsigned*)b;
+    FOTO_TRY(P->alloc(sizeof(int) * (2 * GQ_NB + 1), &b));
+    int* first_d = (int*)b;
+    int* tot_d = first_d + GQ_NB + 1;
+    std::vector<int> htot, hfirst;
+    FOTO_TRY(gq_perm_lists(P, T, P->gq_permv, P->gq_rowmu, first_d, tot_d, htot, hfirst, s));
+    std::vector<GqChunk> ch;
+    std::vector<int> cfirst(GQ_NB + 1);
+    for (int bb = 0; bb < GQ_NB; ++bb) {
+        cfirst[bb] = (int)ch.size();
+        for (int st = 0; st < htot[bb]; st += GQ_PCH)
+            ch.push_back(GqChunk{bb, hfirst[bb] + st, std::min(GQ_PCH, htot[bb] - st), 0});
     }
-    return 0;
+    cfirst[GQ_NB] = (int)ch.size();
+    P->gq_nch = (int)ch.size();
+    FOTO_TRY(P->alloc(sizeof(GqChunk) * std::max<size_t>(1, ch.size()), &b)); P->gq_chunks = (GqChunk*)b;
+    FOTO_TRY(P->alloc(sizeof(int) * (GQ_NB + 1), &b)); P->gq_cfirst = (int*)b;
+    FOTO_TRY(P->alloc(sizeof(double) * GQ_NM * std::max<size_t>(1, ch.size()), &b)); P->gq_ppart = (double*)b;
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->gq_chunks, ch.data(), sizeof(GqChunk) * ch.size(), hipMemcpyHostToDevice, s));
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->gq_cfirst, cfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s));
+    if (P->nyl == P->g.Ny) {
+        k_gq_exact<<<GQ_NB / 64, 64, 0, s>>>(T, P->gq_permv, first_d, tot_d, P->gq_rowmu, 1.0 / P->c1, xmax, P->gq_exact);
+        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_HIP_CHECK(hipStreamSynchronize(s));
+        return 0;
+    }
+    SpecTab TG = T;   // the whole grid
+    TG.y0 = 0;
+    TG.nyl = P->g.Ny;
+    const int grows = P->g.Nt * P->g.Ny;
+    unsigned* gperm = nullptr;
+    double* growmu = nullptr;
+    int* gidx = nullptr;
+    int rc = 0;
+    if (hipMalloc((void**)&gperm, sizeof(unsigned) * (size_t)grows * P->g.Nx) != hipSuccess ||
+        hipMalloc((void**)&growmu, sizeof(double) * grows) != hipSuccess ||
+        hipMalloc((void**)&gidx, sizeof(int) * (2 * GQ_NB + 1)) != hipSuccess) {
+        set_error("gauss exact bins: scratch allocation failed");
+        rc = -1;
+    }
+    if (!rc) rc = gq_perm_lists(P, TG, gperm, growmu, gidx, gidx + GQ_NB + 1, htot, hfirst, s);
+    if (!rc) {
+        k_gq_exact<<<GQ_NB / 64, 64, 0, s>>>(TG, gperm, gidx, gidx + GQ_NB + 1, growmu, 1.0 / P->c1, xmax, P->gq_exact);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+            set_error("gauss exact bins: kernel failed");
+            rc = -1;
+        }
+    }
+    if (gperm) (void)hipFree(gperm);
+    if (growmu) (void)hipFree(growmu);
+    if (gidx) (void)hipFree(gidx);
+    return rc ? -1 : 0;
 }
 
 SpectralPlan::~SpectralPlan() { delete (SpecImpl*)impl; }
@@ -3226,15 +3273,15 @@ static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
         const char* e = getenv("FOTO_GQ_XPERM");
         return e && atoi(e) == 1;
     }();
-    if (P->gq_perm && xperm) {
+    if (xperm) {
         const int nbk = std::max(1, (P->gq_nch + 3) / 4);
         k_gq_xhat_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_tab, P->gq, P->gq_bins,
-                                           P->gq_rowmu, P->c0, 1.0 / P->c1, out);
+                                           P->gq_rowmu, 1.0 / P->c1, out);
         return hipGetLastError();
     }
     const int rows = P->g.Nt * P->nyl;
     const int nb = std::max(1, std::min(cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
-    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins, P->c0, 1.0 / P->c1, out);
+    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins, 1.0 / P->c1, out);
     return hipGetLastError();
 }
 
@@ -3293,23 +3340,11 @@ static int tcol_inverse(SpecImpl* P, double* b, double* x, double rtol, int maxi
 static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     const SpecTab T = P->tab();
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    if (P->gq_perm) {
-        const int nbk = std::max(1, (P->gq_nch + 3) / 4);
-        k_gq_hist_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_bins, P->gq_rowmu,
-                                           P->c0, 1.0 / P->c1, P->gq_ppart);
-        FOTO_HIP_CHECK(hipGetLastError());
-        k_gq_perm_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
-        FOTO_HIP_CHECK(hipGetLastError());
-        if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
-        return 0;
-    }
-    k_gq_hist<<<P->gq_nblk, GQ_HNTH, 0, s>>>(T, P->bh, P->gq_bins, P->c0, 1.0 / P->c1, P->gq_part);
+    const int nbk = std::max(1, (P->gq_nch + 3) / 4);
+    k_gq_hist_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_bins, P->gq_exact,
+                                       P->gq_rowmu, 1.0 / P->c1, P->gq_ppart);
     FOTO_HIP_CHECK(hipGetLastError());
-    const int ngroups = (P->gq_nblk + GQ_RG - 1) / GQ_RG;
-    double* grp = P->gq_part + (size_t)P->gq_nblk * GQ_HIST;
-    k_gq_reduce1<<<ngroups * GQ_HIST / 256, 256, 0, s>>>(P->gq_part, P->gq_nblk, grp);
-    FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_reduce2<<<GQ_HIST / 256, 256, 0, s>>>(grp, ngroups, P->gq_hist + (size_t)P->rank * GQ_HIST);
+    k_gq_perm_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
     return 0;
@@ -3318,11 +3353,11 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
 // the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
 static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->world, P->c0, P->c1, P->gqn);
+    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->gq_exact, P->world, P->r * P->eps, P->c1, P->gqn);
     FOTO_HIP_CHECK(hipGetLastError());
     k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, P->gq);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->c0, P->c1, P->gq_tab);
+    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->r * P->eps, P->c1, P->gq_tab);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
     FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq, P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
