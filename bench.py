@@ -225,6 +225,23 @@ def stream_ceiling(world, pass_us):
                            f"write-through {us[1]:.1f} us per launch"}
 
 
+def stream_ceiling_prox(prox_us):
+    """The fused prox + RHS kernel against the device's stream rate for its traffic
+    (foto_stream_probe4: 4 fields of the grid in, 4 out, 64 B per voxel -- 629 MB at the bench
+    size, beyond the 256 MiB Infinity Cache, so this is the practical HBM rate of that access
+    pattern on this box); stream_frac is what k_prox_rhs keeps of it."""
+    import ctypes
+    from foto import _lib
+    n = NT * NY * NX
+    n -= n % 2
+    us = (ctypes.c_double * 1)()
+    _lib.check(_lib.lib().foto_stream_probe4(n, 10, us))
+    return {"stream_us": round(us[0], 2), "stream_gbs": round(64.0 * n / (us[0] * 1e-6) / 1e9, 1),
+            "stream_frac": round(us[0] / prox_us, 4),
+            "stream_note": f"foto_stream_probe4: 4 x {n} doubles in, 4 out (64 B per voxel), "
+                           f"{us[0]:.1f} us per launch"}
+
+
 def survey_bytes(k):
     """SURVEY.md §8(d) algorithmic bytes of one outer iteration of the literal algorithm:
     (21 + 10 k) N 8 B with k CG iterations."""
@@ -324,11 +341,13 @@ def main():
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": dom, "alg_bytes_per_launch": k["bytes"] / k["n"], "avg_launch_us": round(avg_s * 1e6, 2)}
-            if dom == "spec_cg":
-                try:
+            try:
+                if dom == "spec_cg":
                     roof.update(stream_ceiling(world, avg_s * 1e6))
-                except Exception as e:   # an older library in an A/B run (FOTO_LIB) has no probe
-                    roof["stream_note"] = f"stream probe unavailable: {e}"
+                elif dom == "prox" and world == 1:
+                    roof.update(stream_ceiling_prox(avg_s * 1e6))
+            except Exception as e:   # an older library in an A/B run (FOTO_LIB) has no probe
+                roof["stream_note"] = f"stream probe unavailable: {e}"
 
     line = None
     if rank == 0:

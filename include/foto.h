@@ -183,6 +183,12 @@ int foto_dct(const double* in, int outer, int n, int inner, int inverse, int pat
  * stores, microseconds per launch (best of 3).  n even, n * 8 < 2^31.                   */
 int foto_stream_probe(int64_t n, int reps, double* us);
 
+/* Measurement entry (bench.py): the fused prox + RHS kernel's traffic alone -- read four
+ * n-double fields, write four others (64 B per voxel, the working set well beyond the
+ * Infinity Cache at the bench size), one update per element -- microseconds per launch
+ * (best of 3 over `reps` launches) in us[0].  n even.                                      */
+int foto_stream_probe4(int64_t n, int reps, double* us);
+
 /* ------------------------------------------------------------------ GN baseline
  * classical.GLLOpticalFlow (classical.py:25-130).                                 */
 /* assemble(f1, f2).A @ x and .b (classical.py:68-111)                             */

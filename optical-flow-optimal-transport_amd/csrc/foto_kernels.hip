@@ -727,13 +727,17 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #ifndef FOTO_PR_Y
 #define FOTO_PR_Y 8
 #endif
-constexpr int PR_X = 64, PR_Y = FOTO_PR_Y, PR_NT = PR_X * PR_Y;   // 512 threads (PR_Y 8)
+#ifndef FOTO_PR_X
+#define FOTO_PR_X 64
+#endif
+constexpr int PR_X = FOTO_PR_X, PR_Y = FOTO_PR_Y, PR_NT = PR_X * PR_Y;   // 512 threads (64 x 8)
 constexpr int PR_PW = PR_X + 2, PR_PH = PR_Y + 2;         // stepB region
 constexpr int PR_FW = PR_X + 4, PR_FH = PR_Y + 4;         // phi region
-constexpr int PR_HALO = 2 * PR_PW + 2 * PR_Y;             // 148 ring voxels
+constexpr int PR_HALO = 2 * PR_PW + 2 * PR_Y;             // 148 ring voxels (64 x 8)
 constexpr int PR_FN = PR_FW * PR_FH;                      // 816 phi values per plane
 constexpr int PR_FR = (PR_FN + PR_NT - 1) / PR_NT;        // phi loads per thread per plane
-static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT, "one voxel per thread, ring voxels on the first threads");
+static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT,   // (32 x 16, 16 x 32, 32 x 8: slower, r03)
+              "one voxel per thread, ring voxels on the first threads");
 
 __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_prox_rhs(
         Geo g, const double* __restrict__ phi, const double* __restrict__ mut, const double* __restrict__ mux,

@@ -3796,7 +3796,67 @@ __global__ __launch_bounds__(256) void k_stream_rq(double* __restrict__ r, doubl
         }
     }
 }
+// the prox + RHS traffic: 4 fields in, 4 out, 16 B per lane per field (ping-pong between the
+// two sets of four so every launch streams from HBM)
+__global__ __launch_bounds__(256) void k_stream_4x4(const double* __restrict__ a0, const double* __restrict__ a1,
+                                                    const double* __restrict__ a2, const double* __restrict__ a3,
+                                                    double* __restrict__ b0, double* __restrict__ b1,
+                                                    double* __restrict__ b2, double* __restrict__ b3, int64_t n2, double c) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+        const dbl2 x0 = reinterpret_cast<const dbl2*>(a0)[i], x1 = reinterpret_cast<const dbl2*>(a1)[i];
+        const dbl2 x2 = reinterpret_cast<const dbl2*>(a2)[i], x3 = reinterpret_cast<const dbl2*>(a3)[i];
+        reinterpret_cast<dbl2*>(b0)[i] = x1 + c * x0;
+        reinterpret_cast<dbl2*>(b1)[i] = x2 + c * x0;
+        reinterpret_cast<dbl2*>(b2)[i] = x3 + c * x0;
+        reinterpret_cast<dbl2*>(b3)[i] = x0 - c * (x1 + x2);
+    }
+}
 }  // namespace foto
+
+extern "C" int foto_stream_probe4(int64_t n, int reps, double* us) {
+    using namespace foto;
+    if (!us || n < 2 || n % 2 || reps < 1) {
+        set_error("foto_stream_probe4: bad arguments (n even)");
+        return FOTO_ERR_ARG;
+    }
+    hipStream_t s = nullptr;
+    double* f[8] = {nullptr};
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto body = [&]() -> int {
+        FOTO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        for (int i = 0; i < 8; ++i) FOTO_HIP_CHECK(hipMalloc((void**)&f[i], n * 8));
+        for (int i = 0; i < 8; i += 2) k_stream_fill<<<1024, 256, 0, s>>>(f[i], f[i + 1], n);   // non-zero data
+        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_HIP_CHECK(hipEventCreate(&e0));
+        FOTO_HIP_CHECK(hipEventCreate(&e1));
+        const int nb = 4 * cus_count();
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+            FOTO_HIP_CHECK(hipEventRecord(e0, s));
+            for (int k = 0; k < reps; ++k) {
+                double** A = (k & 1) ? f + 4 : f;
+                double** B = (k & 1) ? f : f + 4;
+                k_stream_4x4<<<nb, 256, 0, s>>>(A[0], A[1], A[2], A[3], B[0], B[1], B[2], B[3], n / 2, 1e-9);
+            }
+            FOTO_HIP_CHECK(hipGetLastError());
+            FOTO_HIP_CHECK(hipEventRecord(e1, s));
+            FOTO_HIP_CHECK(hipEventSynchronize(e1));
+            float t = 0.f;
+            FOTO_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+            best = std::min(best, t);
+        }
+        us[0] = 1e3 * best / reps;
+        return 0;
+    };
+    const int rc = body();
+    if (s) (void)hipStreamSynchronize(s);
+    for (double* p : f)
+        if (p) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    return rc;
+}
 
 extern "C" int foto_stream_probe(int64_t n, int reps, double* us) {
     using namespace foto;

@@ -97,6 +97,7 @@ SIGNATURES = {
     "foto_xfer_calls": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_int64), _I, ctypes.POINTER(_I)]),
     "foto_dct": (_I, [_D, _I, _I, _I, _I, _I, _D]),
     "foto_stream_probe": (_I, [ctypes.c_int64, _I, _D]),
+    "foto_stream_probe4": (_I, [ctypes.c_int64, _I, _D]),
     "foto_gn_apply": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _D, _D]),
     "foto_gn_rhs": (_I, [_D, _D, _I, _I, _D]),
     "foto_gn_solve": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _Dbl, _I, _D, _D, _D, ctypes.POINTER(_I)]),
