@@ -3344,7 +3344,7 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     k_gq_hist_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_bins, P->gq_exact,
                                        P->gq_rowmu, 1.0 / P->c1, P->gq_ppart);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_perm_reduce<<<GQ_HIST / 256, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
+    k_gq_perm_reduce<<<GQ_HIST / 4, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
     return 0;
