@@ -3002,7 +3002,10 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq, sizeof(GqState)));
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
-        FOTO_TRY(P->alloc(2 * GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
+        FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
+        // k_gq_xhat holds the whole table (128 KB) in dynamic LDS, beside its 10 KB bin tables
+        FOTO_HIP_CHECK(hipFuncSetAttribute((const void*)k_gq_xhat, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)GQ_TAB_BYTES));
         FOTO_TRY(P->alloc(sizeof(GqBins), &b)); P->gq_bins = (GqBins*)b;
         k_gq_bins<<<1, 256, 0, s>>>(P->gq_bins);
         FOTO_HIP_CHECK(hipGetLastError());
@@ -3263,22 +3266,9 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
 // plan (forward): single shard, the kernel plans the first pass; sharded, it leaves this rank's INIT
 // moments in gath for the all-gather
 // x^ = Q(lam) b^ (the Gauss-compressed CG's solution table) into a box buffer: one persistent
-// 1024-thread block per CU (the 64 KB table allows one)
+// 1024-thread block per CU (the 128 KB half-bin table allows one)
 static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
     const SpecTab T = P->tab();
-    // FOTO_GQ_XPERM=1: x^ in bin order (k_gq_xhat_perm, coefficients in SGPRs) -- measured
-    // slower than the row-wise LDS-table kernel (66 vs 58 us at 640x480x32: the bin-order
-    // stores land as scattered 8-B writes), kept for A/B runs
-    static const bool xperm = [] {
-        const char* e = getenv("FOTO_GQ_XPERM");
-        return e && atoi(e) == 1;
-    }();
-    if (xperm) {
-        const int nbk = std::max(1, (P->gq_nch + 3) / 4);
-        k_gq_xhat_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_tab, P->gq, P->gq_bins,
-                                           P->gq_rowmu, 1.0 / P->c1, out);
-        return hipGetLastError();
-    }
     const int rows = P->g.Nt * P->nyl;
     const int nb = std::max(1, std::min(cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
     k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins, 1.0 / P->c1, out);
