@@ -1079,15 +1079,18 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double is0 = 1.0 / PB[2 * (M + 1)], is = 1.0 / PB[2 * (M + 1) + 1];
-    // Z_k from X_k, X_{N-k}, X_{M-k}, X_{M+k}, read straight from global (L2-resident lines;
-    // no LDS image of X, so Z is written once and nothing is held in registers across a barrier)
-    using RP = FftRounds<LPB * M>;
+    // Z_k and Z_{M-k} need the same four inputs X_k, X_{N-k}, X_{M-k}, X_{M+k} (V_k and V_{M-k},
+    // conjugated in the other's formula), so one thread makes both: k in [0, M/2], half the
+    // global reads of one Z per thread (L2-resident lines, read straight from global; no LDS
+    // image of X, so Z is written once and nothing is held in registers across a barrier)
+    constexpr int MH = M / 2 + 1;
+    using RP = FftRounds<LPB * MH>;
     double xk[RP::R], xnk[RP::R], xmk[RP::R], xpk[RP::R];   // X_k, X_{N-k}, X_{M-k}, X_{N-M+k}
 #pragma unroll
     for (int j0 = 0; j0 < RP::R; ++j0) {   // all rounds' loads first
         const int idx = tid + 256 * j0;
         int l, k;
-        if (CONTIG) { l = idx / M; k = idx - l * M; }
+        if (CONTIG) { l = idx / MH; k = idx - l * MH; }
         else { k = idx / LPB; l = idx - k * LPB; }
         xk[j0] = xnk[j0] = xmk[j0] = xpk[j0] = 0.0;
         if (RP::ok(idx) && l < f.nl) {
@@ -1103,30 +1106,39 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
         const int idx = tid + 256 * j0;
         if (!RP::ok(idx)) continue;
         int l, k;
-        if (CONTIG) { l = idx / M; k = idx - l * M; }
+        if (CONTIG) { l = idx / MH; k = idx - l * MH; }
         else { k = idx / LPB; l = idx - k * LPB; }
-        double zr = 0.0, zi = 0.0;
+        // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
+        auto V = [&](int j, double xj, double xnj, double& vr, double& vi) {
+            const double yr = xj * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -xnj * is;
+            const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
+            vr = fma(wbr, yr, -wbi * yi);
+            vi = fma(wbr, yi, wbi * yr);
+        };
+        // Z_q from V_q = (ar, ai) and V_{M-q} = (br, bi)
+        auto Zq = [&](int q, double ar, double ai, double br, double bi, double& zr, double& zi) {
+            bi = -bi;                                                  // conj V_{M-q} = V_{q+M}
+            const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_q
+            const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
+            const double war = PA[2 * q], wai = -PA[2 * q + 1];        // e^{+2 pi i q/N}
+            const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_q
+            zr = er - oi;                                              // Z = Ve + i Vo
+            zi = ei + orr;
+        };
+        double z1r = 0.0, z1i = 0.0, z2r = 0.0, z2i = 0.0;
         if (l < f.nl) {
-            // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
-            auto V = [&](int j, double xj, double xnj, double& vr, double& vi) {
-                const double yr = xj * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -xnj * is;
-                const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
-                vr = fma(wbr, yr, -wbi * yi);
-                vi = fma(wbr, yi, wbi * yr);
-            };
             double ar, ai, br, bi;
             V(k, xk[j0], xnk[j0], ar, ai);
             V(M - k, xmk[j0], xpk[j0], br, bi);
-            bi = -bi;                                                  // conj V_{M-k} = V_{k+M}
-            const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_k
-            const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
-            const double war = PA[2 * k], wai = -PA[2 * k + 1];        // e^{+2 pi i k/N}
-            const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_k
-            zr = er - oi;                                              // Z = Ve + i Vo
-            zi = ei + orr;
+            Zq(k, ar, ai, br, bi, z1r, z1i);
+            Zq(M - k, br, bi, ar, ai, z2r, z2i);
         }
-        L[l * LS + 2 * fft_zpos<M2>(k)] = zr;
-        L[l * LS + 2 * fft_zpos<M2>(k) + 1] = zi;
+        L[l * LS + 2 * fft_zpos<M2>(k)] = z1r;
+        L[l * LS + 2 * fft_zpos<M2>(k) + 1] = z1i;
+        if (k != 0 && 2 * k != M) {   // Z_{M-k} (k = 0: M - k = M is no Z index; 2k = M: the same Z)
+            L[l * LS + 2 * fft_zpos<M2>(M - k)] = z2r;
+            L[l * LS + 2 * fft_zpos<M2>(M - k) + 1] = z2i;
+        }
     }
     __syncthreads();
     fft_stage1<M1, M2, true, LPB>(L, TW);
