@@ -63,15 +63,16 @@ def main():
     lines = [f"# compute-only proxy, {NX}x{NY}x{NT}, r={R}, eps={EPS}: per-rank kernel time of W virtual shards on one",
              "# MI355X (HIP events around every launch); COMMUNICATION EXCLUDED (halo / moment all-gathers,",
              "# slab<->box all-to-alls and RCCL latency are not counted) -> an upper bound for W GPUs.",
-             f"# {'W':>2} {'rank ms/it':>10} {'proxy it/s':>10} {'eff':>5} {'CG its':>6} {'pass launches':>13} "
-             f"{'pass ms':>8} {'dct ms':>7} {'prox+rhs ms':>11} {'flow/other':>10}"]
+             f"# {'W':>2} {'rank ms/it':>10} {'proxy it/s':>10} {'eff':>5} {'CG its':>6} {'cg launches':>13} "
+             f"{'cg ms':>8} {'dct ms':>7} {'prox+rhs ms':>11} {'flow/other':>10}"]
     for r in rows:
         k = r["kernels_ms"]
         eff = base / (r["W"] * r["rank_ms"])
         lines.append(f"  {r['W']:>2} {r['rank_ms']:10.3f} {1e3 / r['rank_ms']:10.1f} {eff:5.2f} {r['cg_its']:6.1f} "
                      f"{r['launches'].get('spec_cg', 0):13.1f} {k.get('spec_cg', 0):8.3f} {k.get('dct', 0):7.3f} "
                      f"{k.get('prox', 0) + k.get('rhs', 0):11.3f} {k.get('flow', 0) + k.get('other', 0):10.3f}")
-    lines.append("# pass launches include the deferred solve's no-op margin passes (each a few us).")
+    lines.append("# cg: the CG kernels as timed by the library (mode 3: the Gauss-compressed CG's histogram and "
+                 "node solve groups; mode 2: the s-step passes, incl. a deferred solve's no-op margin passes).")
     lines.append("# rank ms/it = what one rank's GPU computes per outer iteration; one_device_wall_ms in the JSON below is")
     lines.append("# the single device running all W shards in turn (not a scaling number).")
     txt = "\n".join(lines)
