@@ -212,6 +212,18 @@ def color_flow_arrays(u, v, w, h, png):
     Image.fromarray(flow_to_color(np.asarray(u, np.float32), np.asarray(v, np.float32), w, h), "RGB").save(png)
 
 
+def prefetch_frames(ds, seq):
+    """Both frames of a sequence into utils.openGrayscaleImage's decode cache (it keeps the
+    last 4 decodes, i.e. this sequence's and the next one's).  Best effort: a missing or
+    unreadable frame is reported by the sequence's own open."""
+    from utils import openGrayscaleImage
+    for k in (0, 1):
+        try:
+            openGrayscaleImage(ds.frame(seq, k))
+        except Exception:
+            pass
+
+
 def touch(path):
     open(path, "w").close()
 
@@ -343,7 +355,9 @@ def worker(args, rank, world, device):
     mine = shard(jobs(args), rank, world)
     writer = Writer(threads=4)
     try:
-        for ds, seq in mine:
+        for i, (ds, seq) in enumerate(mine):
+            if i + 1 < len(mine):      # decode the next sequence's frames while this one solves
+                writer.pool.submit(prefetch_frames, *mine[i + 1])
             done = run_sequence(ds, seq, args.results, device, args.extra, writer)
             print(f"[rank {rank}/{world}] {ds.name}/{seq}: " + (", ".join(done) if done else "skipped (markers present)"),
                   flush=True)

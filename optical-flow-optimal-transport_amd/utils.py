@@ -10,6 +10,7 @@ Host utilities (image and .flo IO):
   same semantics and quirks as utils.py:25-292.
 """
 import os
+import threading
 import math  # noqa: F401  (kept for API parity with the reference module)
 
 import numpy as np
@@ -20,6 +21,7 @@ from foto import ops as _ops
 
 
 _frames = {}   # (path, mtime_ns, size) -> (f, w, h): the last few decoded frames
+_frames_lock = threading.Lock()   # run.py decodes the next sequence's frames on a pool thread
 
 
 def openGrayscaleImage(inputPathname):
@@ -31,15 +33,17 @@ def openGrayscaleImage(inputPathname):
         key = (os.path.abspath(inputPathname), st.st_mtime_ns, st.st_size)
     except (OSError, TypeError):   # file objects and the like: no caching
         key = None
-    hit = _frames.get(key) if key else None
+    with _frames_lock:
+        hit = _frames.get(key) if key else None
     if hit is None:
         f = np.asarray(Image.open(inputPathname).convert("L"))
         h, w = f.shape
         hit = (f.reshape(-1) / 255, w, h)
         if key:
-            _frames[key] = hit
-            while len(_frames) > 4:
-                del _frames[next(iter(_frames))]
+            with _frames_lock:
+                _frames[key] = hit
+                while len(_frames) > 4:
+                    del _frames[next(iter(_frames))]
     return hit[0].copy(), hit[1], hit[2]
 
 

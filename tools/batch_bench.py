@@ -66,10 +66,16 @@ def main():
     frames, gt = build(args.out, args.seqs)
     res = os.path.join(args.out, "results")
     t, t_wall = time.perf_counter(), time.time()
-    prof = ["-m", "cProfile", "-o", args.cprofile] if args.cprofile else []
-    rc = subprocess.run([sys.executable, *prof, os.path.join(PKG, "run.py"), "run", f"--gpus={args.gpus}",
-                         f"--data={os.path.join(args.out, 'nodata')}", f"--results={res}",
-                         f"--dataset=synthetic={frames}:{gt}"]).returncode
+    run_args = ["run", f"--gpus={args.gpus}", f"--data={os.path.join(args.out, 'nodata')}", f"--results={res}",
+                f"--dataset=synthetic={frames}:{gt}"]
+    if args.cprofile:
+        # run.py's __main__ leaves through os._exit (no stats would be written): profile run.main in-process
+        code = (f"import cProfile, sys; sys.path.insert(0, {PKG!r}); import run; "
+                f"cProfile.run({'run.main(%r)' % run_args!r}, {args.cprofile!r})")
+        cmd = [sys.executable, "-c", code]
+    else:
+        cmd = [sys.executable, os.path.join(PKG, "run.py"), *run_args]
+    rc = subprocess.run(cmd).returncode
     wall, t_end = time.perf_counter() - t, time.time()
     rows = json.load(open(os.path.join(res, "summary.json")))
     print(f"{'sequence':<12} {'algo':<5} {'time s':>7} {'AEE px':>8} {'AAE rad':>8} {'IE':>8}")
