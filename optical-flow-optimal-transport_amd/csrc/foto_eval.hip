@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "foto_internal.h"
@@ -103,29 +104,47 @@ __global__ __launch_bounds__(EV_NT) void k_err_final(int nb, const double* __res
 
 namespace {
 
+// Device buffers of the evaluation calls: grow-only slots kept for the process (a batch worker
+// evaluates every solve at one frame size; hipMalloc / hipFree per call synchronise the device
+// and cost more than the kernels).  One call at a time holds them.
+constexpr int EV_SLOTS = 8;
+std::mutex ev_mu;
+void* ev_slot[EV_SLOTS] = {};
+size_t ev_cap[EV_SLOTS] = {};
+
 struct EvScope {
     hipStream_t s = nullptr;
-    std::vector<void*> bufs;
+    std::unique_lock<std::mutex> lk{ev_mu};
+    int used = 0;
     int init() { return stream_acquire(&s); }
+    int slot(size_t n, double** d) {
+        const size_t bytes = std::max<size_t>(n, 1) * sizeof(double);
+        if (used >= EV_SLOTS) {
+            set_error("evaluation: out of scratch slots");
+            return FOTO_ERR_STATE;
+        }
+        if (ev_cap[used] < bytes) {
+            if (ev_slot[used]) {
+                FOTO_HIP_CHECK(hipStreamSynchronize(s));
+                FOTO_HIP_CHECK(hipFree(ev_slot[used]));
+                ev_slot[used] = nullptr;
+                ev_cap[used] = 0;
+            }
+            FOTO_HIP_CHECK(hipMalloc(&ev_slot[used], bytes));
+            ev_cap[used] = bytes;
+        }
+        *d = (double*)ev_slot[used++];
+        return 0;
+    }
     int up(const double* h, size_t n, double** d) {
         if (!h) { *d = nullptr; return 0; }
-        void* p;
-        FOTO_HIP_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(double)));
-        bufs.push_back(p);
-        *d = (double*)p;
-        FOTO_HIP_CHECK(hipMemcpyAsync(p, h, n * sizeof(double), hipMemcpyHostToDevice, s));
+        FOTO_TRY(slot(n, d));
+        FOTO_HIP_CHECK(hipMemcpyAsync(*d, h, n * sizeof(double), hipMemcpyHostToDevice, s));
         return 0;
     }
-    int dev(size_t n, double** d) {
-        void* p;
-        FOTO_HIP_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(double)));
-        bufs.push_back(p);
-        *d = (double*)p;
-        return 0;
-    }
+    int dev(size_t n, double** d) { return slot(n, d); }
     ~EvScope() {
         if (s) (void)hipStreamSynchronize(s);
-        for (void* p : bufs) (void)hipFree(p);
         stream_release(s);
     }
 };
