@@ -12,8 +12,13 @@ the time axis is sharded into N slabs with RCCL halo exchange (strong scaling: t
 problem on more GPUs); value = outer iterations of that one problem per second.
 
 At N = 1 the line also carries a "gn" object: the GN baseline (classical.py)
-solved on the GPU at 640x480 and 320x240, and the oracle's SuperLU solve of the 320x240 pair on
-one host core beside it.
+solved on the GPU at 640x480 (and 320x240), and the oracle's SuperLU solve of the 640x480 pair
+on one host core beside it (~75 s, run next to the BB CPU baseline on another core).
+
+Multi-GPU runs need no PyTorch: the ranks (launched by torch.distributed.run, which only sets
+RANK / WORLD_SIZE / LOCAL_RANK) meet through files in a directory keyed by the launcher's
+MASTER_PORT and process id (FileRendezvous): rank 0's RCCL unique id, the barriers and the
+max-over-ranks timing.
 
 Prints ONE JSON line on rank 0.
 """
@@ -55,19 +60,6 @@ def parse():
 CPU_K = 2   # outer iterations the CPU baseline runs (BASELINE.md / SURVEY.md §8(d): K = 2 on CPU)
 
 
-def cpu_baseline():
-    """The oracle (numpy/scipy restatement, CSR SpMV + scipy-recurrence CG + vectorised
-    stepB) timed on the first CPU_K outer iterations of the same workload.  Run in a child
-    process pinned to one BLAS/OpenMP thread (the reference path is single-core: scipy's SpMV
-    is single-threaded, SURVEY.md §8(d) measured 8 threads no faster than 1)."""
-    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only"], env=env,
-                         capture_output=True, text=True, timeout=900)
-    if out.returncode != 0:
-        raise RuntimeError("cpu baseline failed: " + out.stderr[-2000:])
-    return json.loads(out.stdout.strip().splitlines()[-1])
-
-
 def cpu_baseline_child():
     sys.path.insert(0, REPO)
     from oracle import foto_oracle as O
@@ -95,7 +87,64 @@ def cpu_baseline_child():
 
 
 GN_W, GN_H, GN_ALPHA, GN_LAMBDA = 640, 480, 0.1, 0.2   # config 3 size, run.sh:103 parameters
-GN_CPU_W, GN_CPU_H = 320, 240                          # bounded CPU sample (spsolve ~13 s here)
+GN_CPU_W, GN_CPU_H = 640, 480                          # the CPU solve at the config's size (spsolve ~75 s)
+GN_SMALL = (320, 240)                                  # second GPU size (latency-bound levels)
+
+
+class FileRendezvous:
+    """Rendezvous of the bench's ranks on one node without torch.distributed: a directory
+    keyed by MASTER_PORT and the launcher's pid (every rank is a child of the same
+    torch.distributed.run agent), files for the RCCL unique id, barriers and per-rank times."""
+
+    def __init__(self, rank, world, timeout=300.0):
+        import tempfile
+        self.rank, self.world, self.timeout, self.n = rank, world, timeout, 0
+        key = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+        self.dir = os.path.join(tempfile.gettempdir(), f"foto_bench_{key}")
+        os.makedirs(self.dir, exist_ok=True)
+
+    def _wait(self, paths):
+        t0 = time.perf_counter()
+        spin = 0
+        while not all(os.path.exists(p) for p in paths):
+            spin += 1
+            if spin > 2000:
+                time.sleep(0.0002)
+            if time.perf_counter() - t0 > self.timeout:
+                raise TimeoutError(f"rendezvous {self.dir}: waited {self.timeout} s for {paths}")
+
+    def _put(self, name, data):
+        tmp = os.path.join(self.dir, f".{name}.{self.rank}.tmp")
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, os.path.join(self.dir, name))
+
+    def broadcast(self, name, data=None):
+        """rank 0's bytes to every rank"""
+        if self.rank == 0:
+            self._put(name, data)
+        p = os.path.join(self.dir, name)
+        self._wait([p])
+        with open(p, "rb") as f:
+            return f.read()
+
+    def barrier(self):
+        self.n += 1
+        self._put(f"bar{self.n}_{self.rank}", b"")
+        self._wait([os.path.join(self.dir, f"bar{self.n}_{g}") for g in range(self.world)])
+
+    def max(self, value):
+        self.n += 1
+        self._put(f"max{self.n}_{self.rank}", repr(float(value)).encode())
+        names = [os.path.join(self.dir, f"max{self.n}_{g}") for g in range(self.world)]
+        self._wait(names)
+        return max(float(open(p).read()) for p in names)
+
+    def close(self):
+        self.barrier()
+        if self.rank == 0:
+            import shutil
+            shutil.rmtree(self.dir, ignore_errors=True)
 
 
 def gn_cpu_child():
@@ -130,17 +179,17 @@ def gn_bytes_per_iteration(w, h):
     return 8 * v
 
 
-def gn_side(with_cpu):
+def gn_side():
     """GN baseline (SURVEY.md §8(d) config 3 stand-in: sinusoid pair, alpha 0.1, lambda 0.2):
-    GPU solve time at 640x480 and at the CPU sample size -- one-shot (foto_gn_solve: plan made,
-    used, destroyed) and with a reused plan (a batch of same-size pairs) -- and the oracle's
-    spsolve beside it."""
+    GPU solve time at 640x480 and 320x240 -- one-shot (foto_gn_solve: plan made, used,
+    destroyed) and with a reused plan (a batch of same-size pairs).  gn_attach_cpu puts the
+    oracle's spsolve of the 640x480 pair (timed in a child process) beside it."""
     from foto import gn
     from foto.synthetic import sinusoid_pair
     out = {"workload": f"GN classical solve, sinusoid pair, alpha={GN_ALPHA}, lambda={GN_LAMBDA}, "
                        f"CG preconditioned by a symmetric multigrid V-cycle to rtol {gn.GN_RTOL}"}
-    for (w, h) in ((GN_W, GN_H), (GN_CPU_W, GN_CPU_H)):
-        f1, f2 = sinusoid_pair(w, h)                  # the CPU sample's pair (at 320x240)
+    for (w, h) in ((GN_W, GN_H), GN_SMALL):
+        f1, f2 = sinusoid_pair(w, h)                  # the CPU sample's pair (at 640x480)
         g1, g2 = sinusoid_pair(w, h, dx=0.7, dy=1.1)  # another pair of the same size
         t = time.perf_counter()
         gn.solve(g1, g2, w, h, GN_ALPHA, GN_LAMBDA)   # makes the cached plan (foto_gn_solve)
@@ -172,19 +221,45 @@ def gn_side(with_cpu):
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                                  "note": "PCG phase: 13 launches per iteration, small levels latency-bound"}})
         out[f"gpu_{w}x{h}"] = rec
-    if with_cpu:
-        env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-        res = subprocess.run([sys.executable, os.path.abspath(__file__), "--gn-cpu-only"], env=env,
-                             capture_output=True, text=True, timeout=600)
-        if res.returncode == 0:
-            cpu_s = json.loads(res.stdout.strip().splitlines()[-1])["solve_s"]
-            gpu_s = out[f"gpu_{GN_CPU_W}x{GN_CPU_H}"]["fresh_pair_ms"] / 1e3
-            out["cpu_baseline"] = {"value_s": round(cpu_s, 3), "kind": "port", "cores": 1,
-                                   "sample": f"oracle spsolve (SuperLU, classical.py:113-130) on the "
-                                             f"{GN_CPU_W}x{GN_CPU_H} pair"}
-            out["speedup_vs_cpu"] = round(cpu_s / gpu_s, 1)
-            out["speedup_note"] = "oracle spsolve vs the GPU's fresh-pair solve at the CPU sample size"
     return out
+
+
+def gn_attach_cpu(out, cpu_s):
+    if cpu_s is not None:
+        gpu_s = out[f"gpu_{GN_CPU_W}x{GN_CPU_H}"]["fresh_pair_ms"] / 1e3
+        out["cpu_baseline"] = {"value_s": round(cpu_s, 3), "kind": "port", "cores": 1,
+                               "sample": f"oracle spsolve (SuperLU, classical.py:113-130) on the "
+                                         f"{GN_CPU_W}x{GN_CPU_H} pair (the config's size)"}
+        out["speedup_vs_cpu"] = round(cpu_s / gpu_s, 1)
+        out["speedup_note"] = (f"oracle spsolve vs the GPU's fresh-pair solve, both at {GN_CPU_W}x{GN_CPU_H}")
+
+
+def start_cpu_children(with_gn):
+    """The CPU baselines as child processes on two different host cores (one thread each):
+    the BB oracle (K = 2 outer iterations) and, with_gn, the GN oracle's spsolve at 640x480."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    cores = sorted(os.sched_getaffinity(0))
+    kids = {}
+    for j, (name, flag) in enumerate((("bb", "--cpu-baseline-only"), ("gn", "--gn-cpu-only"))):
+        if name == "gn" and not with_gn:
+            continue
+        core = cores[(len(cores) - 1 - j) % len(cores)]
+        kids[name] = (subprocess.Popen([sys.executable, os.path.abspath(__file__), flag], env=env,
+                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                       preexec_fn=(lambda c=core: os.sched_setaffinity(0, {c}))), core)
+    return kids
+
+
+def collect_cpu_child(kids, name, timeout=900):
+    if name not in kids:
+        return None
+    p, core = kids[name]
+    out, err = p.communicate(timeout=timeout)
+    if p.returncode != 0:
+        raise RuntimeError(f"cpu baseline {name} failed: " + err[-2000:])
+    res = json.loads(out.strip().splitlines()[-1])
+    res["core"] = core
+    return res
 
 
 def literal_stencil_rate(rho0, rhoT, device, steps=3, warmup=1):
@@ -242,6 +317,38 @@ def stream_ceiling_prox(prox_us):
                            f"{us[0]:.1f} us per launch"}
 
 
+# Algorithmic HBM bytes per voxel of one outer iteration of the default path (cg_mode 3, one
+# GPU): every x / y / t DCT pass reads and writes the grid once (16 B; 3 forward,
+# 3 inverse), the Gauss histogram reads b^ and its 4-B bin-order list entry (12 B), x^ = Q b^
+# reads b^ and writes x^ (16 B), the fused prox + next RHS 64 B.  The node CG, nodes and table
+# move nothing per voxel.
+STEP_BYTES_PER_VOXEL = {"dct_fwd_xyt": 48, "gq_hist": 12, "gq_xhat": 16, "dct_inv_tyx": 48, "prox_rhs": 64}
+
+
+def step_roofline(cg_mode, world, step_s):
+    """The whole outer iteration against HBM peak: the itemised algorithmic bytes above over
+    the measured step time, and the PMC-measured bytes per step (profiles/pmc_traffic.json
+    "_step", written by tools/summarize_profile.py from the same workload)."""
+    if cg_mode != 3 or world != 1:
+        return None
+    n = NX * NY * NT
+    by = sum(STEP_BYTES_PER_VOXEL.values()) * n
+    ach = by / step_s / 1e9
+    out = {"alg_bytes_per_voxel": sum(STEP_BYTES_PER_VOXEL.values()), "items": STEP_BYTES_PER_VOXEL,
+           "alg_bytes": by, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        st = json.load(open(pmc)).get("_step")
+        if st:
+            out["traffic"] = st["hbm_bytes_per_step"]
+            out["traffic_frac_at_this_step_time"] = round(st["hbm_bytes_per_step"] / step_s / 1e9 / HBM_PEAK_GBS, 4)
+            out["traffic_source"] = st.get("source")
+    except Exception:
+        pass
+    return out
+
+
 def survey_bytes(k):
     """SURVEY.md §8(d) algorithmic bytes of one outer iteration of the literal algorithm:
     (21 + 10 k) N 8 B with k CG iterations."""
@@ -262,21 +369,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dist = None
+    rdv = None
     nccl_id = None
     if world > 1:
-        import torch.distributed as dist   # rendezvous / barrier / timing reduction only (gloo, CPU)
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        import foto
-        obj = [None]
+        rdv = FileRendezvous(rank, world)
+        buf = None
         if rank == 0:
             import ctypes
-            buf = ctypes.create_string_buffer(128)
-            foto._lib.check(foto.lib().foto_nccl_unique_id(buf))
-            obj = [bytes(buf.raw)]
-        dist.broadcast_object_list(obj, src=0)
-        nccl_id = obj[0]
+            import foto
+            b = ctypes.create_string_buffer(128)
+            foto._lib.check(foto.lib().foto_nccl_unique_id(b))
+            buf = bytes(b.raw)
+        nccl_id = rdv.broadcast("nccl_id", buf)
 
     from foto.bb import BBSolver
     from foto.synthetic import translating_gaussian
@@ -287,8 +391,8 @@ def main():
 
     def barrier():
         s.sync()
-        if dist is not None:
-            dist.barrier()
+        if rdv is not None:
+            rdv.barrier()
 
     # warmup (untimed)
     s.iterate(args.warmup, 0.0, stop_rules=False)
@@ -297,13 +401,11 @@ def main():
     its_before = len(s.cg_its)
     t0 = time.perf_counter()
     s.iterate(args.steps, 0.0, stop_rules=False)
-    barrier()
+    s.sync()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if rdv is not None:
+        elapsed = rdv.max(elapsed)   # (includes every rank's own device sync)
+        rdv.barrier()
     cg_steps = s.cg_its[its_before:]
     st_timed = s.stats()
 
@@ -383,25 +485,34 @@ def main():
             "kernels": kern,
             "epe": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline()
-            cpu_value = cb["k"] / cb["loop_s"]
-            line["cpu_baseline"] = {"value": round(cpu_value, 6), "unit": "iters/s", "cores": 1,
-                                    "kind": "port", "nproc": os.cpu_count(),
-                                    "affinity": len(os.sched_getaffinity(0)),
-                                    "sample": f"oracle (numpy/scipy CSR + scipy-rule CG + vectorised stepB), first "
-                                              f"{cb['k']} outer iterations of the same 640x480x32 workload "
-                                              f"(CG its {cb['cg_its']}, {cb['loop_s']:.1f} s loop body), "
-                                              f"OMP/BLAS threads 1 (single-core path)"}
-            line["speedup_vs_cpu"] = round(value / cpu_value, 1)
+        if roof is not None:
+            roof["step"] = step_roofline(args.cg_mode, world, elapsed / args.steps)
     s.close()
     if line is not None and world == 1 and args.cg_mode != 0 and not args.no_stencil:
         line["literal_stencil"] = literal_stencil_rate(rho0, rhoT, local_rank)
-    if line is not None and world == 1 and not args.no_gn:
-        line["gn"] = gn_side(with_cpu=not args.no_cpu_baseline)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    # the CPU baselines run after every GPU measurement (no host load beside the timed GPU work),
+    # side by side on two cores
+    kids = {}
+    gn = gn_side() if (line is not None and world == 1 and not args.no_gn) else None
+    if line is not None and world == 1 and not args.no_cpu_baseline:
+        kids = start_cpu_children(with_gn=gn is not None)
+    if gn is not None:
+        gn_cpu = collect_cpu_child(kids, "gn", timeout=1200)
+        gn_attach_cpu(gn, gn_cpu["solve_s"] if gn_cpu else None)
+        line["gn"] = gn
+    if "bb" in kids:
+        cb = collect_cpu_child(kids, "bb")
+        cpu_value = cb["k"] / cb["loop_s"]
+        line["cpu_baseline"] = {"value": round(cpu_value, 6), "unit": "iters/s", "cores": 1,
+                                "kind": "port", "nproc": os.cpu_count(),
+                                "affinity": len(os.sched_getaffinity(0)), "core": cb["core"],
+                                "sample": f"oracle (numpy/scipy CSR + scipy-rule CG + vectorised stepB), first "
+                                          f"{cb['k']} outer iterations of the same 640x480x32 workload "
+                                          f"(CG its {cb['cg_its']}, {cb['loop_s']:.1f} s loop body), "
+                                          f"OMP/BLAS threads 1 (single-core path), pinned to one core"}
+        line["speedup_vs_cpu"] = round(line["value"] / cpu_value, 1)
+    if rdv is not None:
+        rdv.close()
     if line is not None:
         print(json.dumps(line))
 

@@ -6,7 +6,8 @@ update, criterion) and the flow extraction run in libfoto.so (HIP, gfx950).  The
 is selected by ``cg_mode`` (env FOTO_CG_MODE): 3 = CG on the Gauss-compressed spectral
 measure of the right-hand side (default; csrc/foto_gauss.inc), 2 = s-step CG in the DCT-II
 eigenbasis of A, 1 = one-pass CG in that basis, 0 = 7-point stencil CG.  All follow scipy's
-CG recurrence and stopping rule; every mode runs time-sharded over GPUs.
+CG recurrence and stopping rule.  Modes 0, 2 and 3 run time-sharded over GPUs; mode 1 is
+single-GPU only (include/foto.h).
 """
 import os
 
@@ -28,12 +29,21 @@ def solve_benamou_brenier_step(mu, q, rho0, rhoT, r, A, div, Nt, Nx, Ny, dt, dx,
     if (dt, dx, dy) != (1, 1, 1):
         raise NotImplementedError("the GPU path implements the reference's dt = dx = dy = 1")
     N = Nt * Nx * Ny
+    if A.shape != (N, N):
+        raise NotImplementedError(f"A has shape {A.shape}, expected ({N}, {N})")
     d0 = float(A.diagonal()[0])          # corner voxel: r * (3 + eps)
     eps = d0 / r - 3.0
-    probe = np.zeros(N)
-    probe[0] = 1.0
-    if not np.allclose(A @ probe, _ops.apply_A(probe, Nt, Nx, Ny, r, eps), rtol=1e-12, atol=1e-14):
-        raise NotImplementedError("A is not -r*laplacian_st + r*eps*I on this grid")
+    # A must be exactly the operator the GPU applies: compare on random vectors (any other
+    # matrix -- a different stencil, a changed entry anywhere -- fails with probability 1) and
+    # the stored entries against the 7-point pattern (every voxel: itself + its neighbours)
+    rng = np.random.default_rng(12345)
+    for _ in range(2):
+        x = rng.standard_normal(N)
+        if not np.allclose(A @ x, _ops.apply_A(x, Nt, Nx, Ny, r, eps), rtol=1e-12, atol=1e-12 * abs(r)):
+            raise NotImplementedError("A is not -r*laplacian_st + r*eps*I on this grid")
+    edges = (Nt - 1) * Nx * Ny + Nt * (Nx - 1) * Ny + Nt * Nx * (Ny - 1)
+    if hasattr(A, "count_nonzero") and A.count_nonzero() > N + 2 * edges:
+        raise NotImplementedError("A has entries outside the 7-point space-time stencil")
     F = _ops.bb_rhs(mu, q, rho0, rhoT, r, Nt, Nx, Ny)
     u, info, _ = _ops.cg(F, Nt, Nx, Ny, r, eps, rtol=1e-6, maxiter=1000, mode=_default_mode())
     if info > 0:

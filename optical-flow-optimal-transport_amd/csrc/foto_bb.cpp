@@ -34,7 +34,10 @@ void set_error(const char* fmt, ...) {
 
 static std::mutex g_pool_mu;
 static std::vector<std::pair<int, hipStream_t>> g_pool;   // (device, stream) free list
+static std::vector<std::pair<hipStream_t, int>> g_live;   // streams handed out, with their device
 
+// a stream of the current device; stream_release files it under the device it was created on
+// (not the device current at release: a context on device 1 closed while device 0 is current)
 int stream_acquire(hipStream_t* out) {
     int dev = 0;
     FOTO_HIP_CHECK(hipGetDevice(&dev));
@@ -44,19 +47,32 @@ int stream_acquire(hipStream_t* out) {
             if (g_pool[i].first == dev) {
                 *out = g_pool[i].second;
                 g_pool.erase(g_pool.begin() + i);
+                g_live.push_back({*out, dev});
                 return 0;
             }
     }
     FOTO_HIP_CHECK(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_live.push_back({*out, dev});
     return 0;
 }
 
 void stream_release(hipStream_t s) {
     if (!s) return;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back({dev, s});
+    for (size_t i = 0; i < g_live.size(); ++i)
+        if (g_live[i].first == s) {
+            g_pool.push_back({g_live[i].second, s});
+            g_live.erase(g_live.begin() + i);
+            return;
+        }
+}
+
+int stream_device(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const auto& e : g_live)
+        if (e.first == s) return e.second;
+    return -1;
 }
 
 #define FOTO_NCCL_CHECK(call)                                                                 \
@@ -77,7 +93,9 @@ struct Shard {
     double* mu[3] = {nullptr, nullptr, nullptr};
     double* q[3] = {nullptr, nullptr, nullptr};
     double* nu[3] = {nullptr, nullptr, nullptr};   // second mu buffer of the fused prox + RHS
+    double* xi[3] = {nullptr, nullptr, nullptr};   // third mu buffer (two outer iterations in flight)
     double* phi = nullptr;   // CG iterate x
+    double* phi_alt = nullptr;   // the other phi of the pipelined loop
     double* rv = nullptr;    // CG residual (starts as F)
     double* p[2] = {nullptr, nullptr};
     double* rho0 = nullptr;
@@ -133,33 +151,56 @@ struct foto_bb_ctx {
     hipStream_t s = nullptr;
     std::vector<std::unique_ptr<Shard>> sh;   // local shards
     CGScal* hS = nullptr;                     // pinned host mirror of shard 0's CG scalars
-    double* hgath = nullptr;                  // pinned host mirror of gath
     int last_cg = 0;
     int last_passes = 0;   // s-step passes of the previous sharded spectral solve
-    // the outer iteration on the stream (outer_enqueue -> outer_complete)
-    int enq_its = 0, enq_info = 0;
-    SpectralPlan* enq_dsp = nullptr;
     int have_phi = 0;
     // single shard: prox fused with the next RHS (k_prox_rhs); F in rv is then produced by
-    // the previous outer iteration (f_ready), mu ping-pongs between Shard::mu and Shard::nu
+    // the previous outer iteration (f_ready), mu rotates through Shard::mu / nu (/ xi)
     bool fuse = false;
     bool f_ready = false;
     double* fz_src[3] = {nullptr, nullptr, nullptr};   // the last fused launch's mu in / out
     double* fz_dst[3] = {nullptr, nullptr, nullptr};
+    // Two outer iterations in flight (single shard, fused, Gauss CG; FOTO_PIPE=0: one): the
+    // host enqueues iteration i + 1 before it waits for iteration i's crit, so the GPU never
+    // idles while the host wakes up and launches.  mu rotates through three buffers and phi
+    // alternates between two, so an iteration the stop rules turn out not to want is dropped
+    // (rollback) with iteration i's state intact; a failed Gauss solve is redone after its
+    // successor, which its done-flag chain kept from touching the state, is dropped.
+    bool pipe = false;
+    struct Enq {            // an outer iteration on the stream (outer_tail -> outer_complete)
+        int par = 0;        // its event / readback slot
+        SpectralPlan* dsp = nullptr;   // deferred solve to finish
+        int its = 0, info = 0;         // a synchronous solve's result
+        size_t kmark = 0;              // KTimer mark before its launches
+        // host state before it (restored by a rollback)
+        double* mu[3];
+        double* nu[3];
+        double* xi[3];
+        double* phi;
+        double* phi_alt;
+        double* fz_src[3];
+        double* fz_dst[3];
+        bool f_ready;
+        int hpar;
+    };
+    std::vector<Enq> inflight;   // oldest first
     // bookkeeping
     double prev_crit = -1;
     foto_bb_stats st{};
     KTimer kt;
-    hipEvent_t ph[4] = {nullptr, nullptr, nullptr, nullptr};   // phase boundaries (rhs | cg | prox)
-    hipEvent_t phr[2] = {nullptr, nullptr};   // RHS start, by parity (the next RHS may be enqueued early)
-    int hpar = 0, tail_par = 0;
+    hipEvent_t ph[2][4] = {};      // per slot: RHS start | CG start | prox start | crit readback
+    hipEvent_t fl[2] = {};         // flow extraction
+    double* hgath[2] = {nullptr, nullptr};   // pinned host mirrors of gath, per slot
+    int hpar = 0;                  // slot of the last head
     ~foto_bb_ctx() {
+        if (s) (void)hipStreamSynchronize(s);   // (before the shards free their buffers)
         sh.clear();
         if (nc) (void)ncclCommDestroy(nc);
         if (hS) (void)hipHostFree(hS);
-        if (hgath) (void)hipHostFree(hgath);
-        for (auto e : ph) if (e) (void)hipEventDestroy(e);
-        for (auto e : phr) if (e) (void)hipEventDestroy(e);
+        for (double* h : hgath) if (h) (void)hipHostFree(h);
+        for (auto& p : ph)
+            for (auto e : p) if (e) (void)hipEventDestroy(e);
+        for (auto e : fl) if (e) (void)hipEventDestroy(e);
         if (s) {
             (void)hipStreamSynchronize(s);
             stream_release(s);
@@ -238,9 +279,10 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     FOTO_TRY(stream_acquire(&c->s));
     FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hS, sizeof(CGScal)));
     const int W = c->W;
-    FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hgath, sizeof(double) * 4 * W));
-    for (auto& e : c->ph) FOTO_HIP_CHECK(hipEventCreate(&e));
-    for (auto& e : c->phr) FOTO_HIP_CHECK(hipEventCreate(&e));
+    for (double*& h : c->hgath) FOTO_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(double) * 4 * W));
+    for (auto& p : c->ph)
+        for (auto& e : p) FOTO_HIP_CHECK(hipEventCreate(&e));
+    for (auto& e : c->fl) FOTO_HIP_CHECK(hipEventCreate(&e));
     if (c->rccl) {
         ncclUniqueId id;
         memcpy(&id, c->o.nccl_id, sizeof(id));
@@ -250,6 +292,8 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     {
         const char* e = getenv("FOTO_FUSE_PR");   // 0: separate k_prox / k_rhs (A/B runs)
         c->fuse = (W == 1) && !(e && atoi(e) == 0);
+        const char* pe = getenv("FOTO_PIPE");   // 0: one outer iteration in flight (A/B runs)
+        c->pipe = c->fuse && c->o.cg_mode == 3 && !(pe && atoi(pe) == 0);
     }
     for (int j = 0; j < nlocal; ++j) {
         auto sp = std::make_unique<Shard>();
@@ -263,6 +307,10 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         for (int f = 0; f < 3; ++f) { FOTO_TRY(s.alloc_field(&s.mu[f], c->s)); FOTO_TRY(s.alloc_field(&s.q[f], c->s)); }
         if (c->fuse)
             for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.nu[f], c->s));
+        if (c->pipe) {
+            for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.xi[f], c->s));
+            FOTO_TRY(s.alloc_field(&s.phi_alt, c->s));
+        }
         FOTO_TRY(s.alloc_field(&s.phi, c->s));
         FOTO_TRY(s.alloc_field(&s.rv, c->s));
         FOTO_TRY(s.alloc_field(&s.p[0], c->s));
@@ -292,6 +340,8 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         }
         c->sh.push_back(std::move(sp));
     }
+    // the Gauss CG may fall back to the s-step CG for boxes its voxel list cannot pack
+    if (c->pipe && !(c->sh[0]->spec && c->sh[0]->spec->gauss())) c->pipe = false;
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     return 0;
 }
@@ -455,17 +505,17 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 
 // ----------------------------------------------------------------------------- outer iteration
 
-// One outer iteration in two halves.  outer_enqueue puts the iteration's work on the stream
-// (a non-deferred CG solve waits for itself inside); outer_complete waits for the crit
-// readback, finishes a deferred solve and computes crit.  The enqueue half is itself split:
-// outer_head (halos, RHS) only writes F and, for a single spectral shard, foto_bb_iterate
-// puts the next iteration's head on the stream before waiting for this iteration's crit, so
-// the GPU computes the RHS while the host wakes up (the stop rules can still end the run there:
-// F is scratch; a CG redo re-runs the head).  The host callback runs after the next
-// iteration is enqueued.
+// One outer iteration in two halves.  outer_head + outer_tail put the iteration's work on the
+// stream (a non-deferred CG solve waits for itself inside) and push an Enq record;
+// outer_complete waits for the oldest record's crit readback, finishes its deferred solve and
+// computes crit.  outer_head (halos, RHS) only writes F.  With one iteration in flight, a single
+// spectral shard gets the next iteration's head on the stream before the host waits for this
+// iteration's crit (the stop rules can still end the run there: F is scratch; a CG redo re-runs
+// the head).  With two in flight (c->pipe) the whole next iteration is enqueued first.  The
+// host callback runs after the next iteration is enqueued.
 static int outer_head(foto_bb_ctx* c) {
     c->hpar ^= 1;
-    FOTO_HIP_CHECK(hipEventRecord(c->phr[c->hpar], c->s));
+    FOTO_HIP_CHECK(hipEventRecord(c->ph[c->hpar][0], c->s));
     // the previous iteration's k_prox_rhs wrote F (and F.F).  (Enqueuing the next solve's x-DCT
     // here, ahead of the crit wait, measured no faster: 457 vs 457 it/s same box.)
     if (c->fuse && c->f_ready) return 0;
@@ -495,66 +545,127 @@ static int prox_rhs(foto_bb_ctx* c, const int* guard) {
     return 0;
 }
 
-static int outer_tail(foto_bb_ctx* c) {
+// kmark: the KTimer mark taken before this iteration's head
+static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     const int W = c->W;
-    int* cg_iters = &c->enq_its;
-    int* cg_info = &c->enq_info;
-    c->tail_par = c->hpar;
+    Shard& s0 = *c->sh[0];
+    foto_bb_ctx::Enq e;
+    e.par = c->hpar;
+    e.kmark = kmark;
+    for (int f = 0; f < 3; ++f) {
+        e.mu[f] = s0.mu[f]; e.nu[f] = s0.nu[f]; e.xi[f] = s0.xi[f];
+        e.fz_src[f] = c->fz_src[f]; e.fz_dst[f] = c->fz_dst[f];
+    }
+    e.phi = s0.phi;
+    e.phi_alt = s0.phi_alt;
+    e.f_ready = c->f_ready;
+    e.hpar = c->hpar ^ 1;   // (before this iteration's head)
+    hipEvent_t* ph = c->ph[e.par];
     // phase boundaries are recorded, not waited on: the one host wait per outer iteration
     // is the crit readback below (a wait here idled the GPU for the host's wake-up)
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    // Single shard, spectral s-step: once a solve has fixed the pass count, the solve is
-    // enqueued without a host wait and prox follows behind it, guarded by the CG's done flag;
-    // the one sync below (crit) then also delivers the CG result.  A solve that needs more
-    // passes than predicted (rare: the count changes by 0-1 between outer iterations) is
-    // finished after that sync, and prox re-runs (FOTO_CG_DEFER=0: always wait for the CG).
+    FOTO_HIP_CHECK(hipEventRecord(ph[1], c->s));
+    // Single shard, spectral: the solve is enqueued without a host wait and prox follows behind
+    // it, guarded by the CG's done flag; the one sync (crit) then also delivers the CG result.
+    // A solve that needs more work (s-step: more passes than predicted; Gauss: K beyond the
+    // table) is finished after that sync, and prox re-runs (FOTO_CG_DEFER=0: always wait).
     const char* de = getenv("FOTO_CG_DEFER");
     const bool defer_on = !(de && atoi(de) == 0);
-    SpectralPlan* dsp = (defer_on && W == 1 && c->o.cg_mode != 0 && c->sh[0]->spec && c->sh[0]->spec->deferrable())
-                            ? c->sh[0]->spec.get()
+    SpectralPlan* dsp = (defer_on && W == 1 && c->o.cg_mode != 0 && s0.spec && s0.spec->deferrable())
+                            ? s0.spec.get()
                             : nullptr;
-    if (dsp) {
-        Shard& s = *c->sh[0];
-        FOTO_TRY(dsp->solve_deferred(s.rv, s.phi, c->o.cg_rtol, c->o.cg_maxiter, &c->kt, c->s));
-    } else {
-        FOTO_TRY(cg_solve(c, cg_iters, cg_info));
+    if (c->pipe && !dsp) {
+        set_error("outer iteration: the pipelined loop needs a deferrable Gauss solve");
+        return FOTO_ERR_STATE;
     }
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[2], c->s));
+    if (c->pipe) std::swap(s0.phi, s0.phi_alt);   // this iteration's phi; the last one's stays intact
+    if (dsp) {
+        FOTO_TRY(dsp->solve_deferred(s0.rv, s0.phi, c->o.cg_rtol, c->o.cg_maxiter, &c->kt, c->s));
+    } else {
+        FOTO_TRY(cg_solve(c, &e.its, &e.info));
+    }
+    FOTO_HIP_CHECK(hipEventRecord(ph[2], c->s));
     c->have_phi = 1;
 
     if (c->fuse) {
         // prox + the next iteration's RHS: mu -> nu, F -> rv; then nu is the current mu
-        Shard& s = *c->sh[0];
-        for (int f = 0; f < 3; ++f) { c->fz_src[f] = s.mu[f]; c->fz_dst[f] = s.nu[f]; }
+        // (pipelined: mu -> nu -> xi -> mu rotate, so the mu before this iteration survives it)
+        for (int f = 0; f < 3; ++f) { c->fz_src[f] = s0.mu[f]; c->fz_dst[f] = s0.nu[f]; }
         FOTO_TRY(prox_rhs(c, dsp ? dsp->done_flag() : nullptr));
-        for (int f = 0; f < 3; ++f) std::swap(s.mu[f], s.nu[f]);
+        for (int f = 0; f < 3; ++f) {
+            if (c->pipe) {
+                double* m = s0.mu[f];
+                s0.mu[f] = s0.nu[f];
+                s0.nu[f] = s0.xi[f];
+                s0.xi[f] = m;
+            } else {
+                std::swap(s0.mu[f], s0.nu[f]);
+            }
+        }
         c->f_ready = true;
     } else {
         FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
         for (auto& sp : c->sh) {
             Shard& s = *sp;
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
-            hipEvent_t e = c->kt.start(c->s);
+            hipEvent_t t = c->kt.start(c->s);
             FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
                                        s.gath_crit(W), s.rank, c->s, dsp ? dsp->done_flag() : nullptr));
-            c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+            c->kt.stop(t, c->s, FOTO_K_PROX, 80.0 * nv);
         }
     }
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
-    FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, c->sh[0]->gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
-    c->enq_dsp = dsp;
+    FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s0.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+    FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
+    e.dsp = dsp;
+    c->inflight.push_back(e);
+    return 0;
+}
+
+// Drop the newest enqueued outer iteration (pipelined loop only): wait for the stream, forget
+// its solve and its timings, and put the host state back as it was before it.  F of the last
+// kept iteration was overwritten by the dropped one's prox, so the next head recomputes it from
+// q, itself recomputed from that iteration's phi and the mu before it (both intact).
+static int rollback(foto_bb_ctx* c) {
+    if (c->inflight.empty()) return 0;
+    const foto_bb_ctx::Enq e = c->inflight.back();
+    c->inflight.pop_back();
+    FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    Shard& s0 = *c->sh[0];
+    if (e.dsp) FOTO_TRY(e.dsp->drop_newest(c->s));
+    c->kt.discard_from(e.kmark);
+    for (int f = 0; f < 3; ++f) {
+        s0.mu[f] = e.mu[f]; s0.nu[f] = e.nu[f]; s0.xi[f] = e.xi[f];
+        c->fz_src[f] = e.fz_src[f]; c->fz_dst[f] = e.fz_dst[f];
+    }
+    s0.phi = e.phi;
+    s0.phi_alt = e.phi_alt;
+    c->hpar = e.hpar;
+    if (e.f_ready && c->fz_src[0]) {
+        // q of the kept iteration (stepB of its phi and the mu before it), for the next head's RHS
+        FOTO_HIP_CHECK(launch_q_from_phi(s0.g, s0.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], s0.q[0], s0.q[1],
+                                         s0.q[2], c->r, c->s));
+    }
+    c->f_ready = false;   // (a dropped first iteration leaves mu, q as they were: the head recomputes F)
     return 0;
 }
 
 static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_info) {
     const int W = c->W;
-    SpectralPlan* dsp = c->enq_dsp;
-    c->enq_dsp = nullptr;
-    *cg_iters = c->enq_its;
-    *cg_info = c->enq_info;
-    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
+    if (c->inflight.empty()) {
+        set_error("outer iteration: nothing in flight");
+        return FOTO_ERR_STATE;
+    }
+    const foto_bb_ctx::Enq e = c->inflight.front();
+    c->inflight.erase(c->inflight.begin());
+    SpectralPlan* dsp = e.dsp;
+    *cg_iters = e.its;
+    *cg_info = e.info;
+    hipEvent_t* ph = c->ph[e.par];
+    FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
     if (dsp) {
+        // a failed solve is redone once the iteration behind it (whose prox its done-flag chain
+        // skipped) is dropped; the loop enqueues that iteration again
+        if (!c->inflight.empty() && dsp->oldest_needs_redo()) FOTO_TRY(rollback(c));
         int redo = 0;
         FOTO_TRY(dsp->finish(cg_iters, cg_info, &redo, &c->kt, c->s));
         c->last_cg = *cg_iters;
@@ -564,28 +675,30 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             c->kt.discard_last(FOTO_K_PROX, 1);
             if (c->fuse) {
                 FOTO_TRY(prox_rhs(c, nullptr));
+                c->f_ready = true;   // (a rollback before the redo had cleared it)
             } else {
-                hipEvent_t e = c->kt.start(c->s);
+                hipEvent_t t = c->kt.start(c->s);
                 FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r,
                                            s.rb, s.gath_crit(W), s.rank, c->s));
-                c->kt.stop(e, c->s, FOTO_K_PROX, 80.0 * nv);
+                c->kt.stop(t, c->s, FOTO_K_PROX, 80.0 * nv);
             }
-            FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath, s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipEventRecord(c->ph[3], c->s));
-            FOTO_HIP_CHECK(hipEventSynchronize(c->ph[3]));
+            FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
+            FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
             c->st.cg_redo += 1;
         }
     }
     float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, c->phr[c->tail_par], c->ph[1]));
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, c->ph[1], c->ph[2]));
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, c->ph[2], c->ph[3]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, ph[0], ph[1]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, ph[1], ph[2]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, ph[2], ph[3]));
     c->st.ms_rhs += t_rhs;
     c->st.ms_cg += t_cg;
     c->st.ms_prox += t_prox;
 
+    const double* hg = c->hgath[e.par];
     double num = 0.0, den = 0.0;
-    for (int g = 0; g < W; ++g) { num += c->hgath[2 * W + 2 * g]; den += c->hgath[2 * W + 2 * g + 1]; }
+    for (int g = 0; g < W; ++g) { num += hg[2 * W + 2 * g]; den += hg[2 * W + 2 * g + 1]; }
     *crit = std::sqrt(num / (den + 1e-10));
     c->st.outer_iters += 1;
     c->st.cg_iters_total += *cg_iters;
@@ -599,7 +712,7 @@ static int flow(foto_bb_ctx* c, double* u, double* v, double* m) {
         return FOTO_ERR_STATE;
     }
     const int W = c->W;
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[0], c->s));
+    FOTO_HIP_CHECK(hipEventRecord(c->fl[0], c->s));
     // Trajectories relay rank to rank: rank j runs the steps of its planes, then its
     // positions travel to rank j + 1; the last rank finishes (u, v, m) and delivers them to
     // rank 0.  The same transfer lists for both transports (exchange()).
@@ -634,10 +747,10 @@ static int flow(foto_bb_ctx* c, double* u, double* v, double* m) {
             FOTO_HIP_CHECK(hipMemcpyAsync(m, s0->fm, nxy * sizeof(double), hipMemcpyDeviceToHost, c->s));
         }
     }
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[1], c->s));
-    FOTO_HIP_CHECK(hipEventSynchronize(c->ph[1]));
+    FOTO_HIP_CHECK(hipEventRecord(c->fl[1], c->s));
+    FOTO_HIP_CHECK(hipEventSynchronize(c->fl[1]));
     float t = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t, c->ph[0], c->ph[1]));
+    FOTO_HIP_CHECK(hipEventElapsedTime(&t, c->fl[0], c->fl[1]));
     c->st.ms_flow += t;
     return 0;
 }
@@ -747,36 +860,70 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
 int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rules, foto_bb_iter_cb cb, void* user,
                     int* iters_done) {
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
+    if (!c->inflight.empty()) { set_error("foto_bb_iterate: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
     int done = 0;
     int stopped = 0;
-    // the next RHS goes on the stream early for a single spectral shard (see outer_head)
+    auto stop_test = [&](double crit) {
+        const double prev = c->prev_crit;
+        c->prev_crit = crit;
+        if (!use_stop_rules) return 0;
+        if (crit <= tol) return 1;
+        return (prev >= 0 && std::fabs(prev - crit) < 1e-5) ? 1 : 0;
+    };
+    if (c->pipe) {
+        // two outer iterations in flight: iteration i + 1 is on the stream before the host
+        // waits for iteration i (dropped again if the stop rules end the run at i)
+        int enq = 0;
+        for (int i = 0; i < max_iters; ++i) {
+            while ((int)c->inflight.size() < 2 && enq < max_iters) {
+                const size_t km = c->kt.mark();
+                FOTO_TRY(outer_head(c));
+                FOTO_TRY(outer_tail(c, km));
+                ++enq;
+            }
+            double crit;
+            int its, info;
+            const size_t n_before = c->inflight.size();
+            FOTO_TRY(outer_complete(c, &crit, &its, &info));
+            if (c->inflight.size() + 1 < n_before) --enq;   // a redo dropped the iteration behind
+            ++done;
+            stopped = stop_test(crit);
+            if (stopped && !c->inflight.empty()) {
+                FOTO_TRY(rollback(c));
+                --enq;
+            }
+            c->kt.resolve_upto(c->inflight.empty() ? c->kt.mark() : c->inflight.front().kmark);
+            if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
+            if (stopped) break;
+        }
+        if (iters_done) *iters_done = done;
+        return stopped;
+    }
+    // one outer iteration in flight; the next RHS goes on the stream early for a single
+    // spectral shard (see outer_head)
     const bool early = c->W == 1 && c->o.cg_mode != 0;
     if (max_iters > 0) {
+        const size_t km = c->kt.mark();
         FOTO_TRY(outer_head(c));
-        FOTO_TRY(outer_tail(c));
+        FOTO_TRY(outer_tail(c, km));
     }
     for (int i = 0; i < max_iters; ++i) {
         double crit;
         int its, info;
-        const size_t mark = c->kt.pending();
+        const size_t mark = c->kt.mark();
         const bool head_early = early && i + 1 < max_iters;
         if (head_early) FOTO_TRY(outer_head(c));
         const int redo0 = c->st.cg_redo;
         FOTO_TRY(outer_complete(c, &crit, &its, &info));
         ++done;
-        const double prev = c->prev_crit;
-        c->prev_crit = crit;
-        if (use_stop_rules) {
-            if (crit <= tol) stopped = 1;
-            else if (prev >= 0 && std::fabs(prev - crit) < 1e-5) stopped = 1;
-        }
+        stopped = stop_test(crit);
         // the next iteration goes on the stream before the host's bookkeeping for this one
         if (!stopped && i + 1 < max_iters) {
             // a redo re-ran this iteration's prox after the early head read mu, q: head again
             if (!head_early || c->st.cg_redo != redo0) FOTO_TRY(outer_head(c));
-            FOTO_TRY(outer_tail(c));
+            FOTO_TRY(outer_tail(c, mark));
         }
-        c->kt.resolve_first(mark);
+        c->kt.resolve_upto(mark);
         if (cb) cb(user, c->st.outer_iters - 1, crit, its, info);
         if (stopped) break;
     }
@@ -786,14 +933,14 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
 
 int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     if (!c || !rho0 || !rhoT) { set_error("null argument"); return FOTO_ERR_ARG; }
-    if (c->enq_dsp) { set_error("foto_bb_reset: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
+    if (!c->inflight.empty()) { set_error("foto_bb_reset: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
     const int64_t nxy = (int64_t)c->Nx * c->Ny;
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     for (auto& sp : c->sh) {
         Shard& s = *sp;
         const size_t bytes = (size_t)(s.g.nloc + 2) * (size_t)nxy * sizeof(double);
         double* fields[] = {s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], s.nu[0], s.nu[1], s.nu[2],
-                            s.phi, s.rv, s.p[0], s.p[1]};
+                            s.xi[0], s.xi[1], s.xi[2], s.phi, s.phi_alt, s.rv, s.p[0], s.p[1]};
         for (double* f : fields)   // as ctx_init leaves them: zero, halo planes included
             if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - nxy, 0, bytes, c->s));
         FOTO_HIP_CHECK(hipMemsetAsync(s.gath, 0, sizeof(double) * 4 * c->W, c->s));
@@ -806,7 +953,6 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     }
     c->last_cg = 0;
     c->last_passes = 0;
-    c->enq_its = c->enq_info = 0;
     c->have_phi = 0;
     c->f_ready = false;
     for (int f = 0; f < 3; ++f) c->fz_src[f] = c->fz_dst[f] = nullptr;
@@ -814,7 +960,7 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     c->st = foto_bb_stats{};
     c->kt.resolve();
     c->kt.reset();
-    c->hpar = c->tail_par = 0;
+    c->hpar = 0;
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     return 0;
 }

@@ -108,32 +108,46 @@ namespace {
 // evaluates every solve at one frame size; hipMalloc / hipFree per call synchronise the device
 // and cost more than the kernels).  One call at a time holds them.
 constexpr int EV_SLOTS = 8;
+struct EvSlots {
+    void* p[EV_SLOTS] = {};
+    size_t cap[EV_SLOTS] = {};
+};
 std::mutex ev_mu;
-void* ev_slot[EV_SLOTS] = {};
-size_t ev_cap[EV_SLOTS] = {};
+std::vector<EvSlots> ev_dev;   // per device (a slot is only valid on the device it was made on)
 
 struct EvScope {
     hipStream_t s = nullptr;
     std::unique_lock<std::mutex> lk{ev_mu};
+    EvSlots* sl = nullptr;
     int used = 0;
-    int init() { return stream_acquire(&s); }
+    int init() {
+        FOTO_TRY(stream_acquire(&s));
+        const int dev = stream_device(s);
+        if (dev < 0) {
+            set_error("evaluation: stream without a device");
+            return FOTO_ERR_STATE;
+        }
+        if ((int)ev_dev.size() <= dev) ev_dev.resize(dev + 1);
+        sl = &ev_dev[dev];
+        return 0;
+    }
     int slot(size_t n, double** d) {
         const size_t bytes = std::max<size_t>(n, 1) * sizeof(double);
         if (used >= EV_SLOTS) {
             set_error("evaluation: out of scratch slots");
             return FOTO_ERR_STATE;
         }
-        if (ev_cap[used] < bytes) {
-            if (ev_slot[used]) {
+        if (sl->cap[used] < bytes) {
+            if (sl->p[used]) {
                 FOTO_HIP_CHECK(hipStreamSynchronize(s));
-                FOTO_HIP_CHECK(hipFree(ev_slot[used]));
-                ev_slot[used] = nullptr;
-                ev_cap[used] = 0;
+                FOTO_HIP_CHECK(hipFree(sl->p[used]));
+                sl->p[used] = nullptr;
+                sl->cap[used] = 0;
             }
-            FOTO_HIP_CHECK(hipMalloc(&ev_slot[used], bytes));
-            ev_cap[used] = bytes;
+            FOTO_HIP_CHECK(hipMalloc(&sl->p[used], bytes));
+            sl->cap[used] = bytes;
         }
-        *d = (double*)ev_slot[used++];
+        *d = (double*)sl->p[used++];
         return 0;
     }
     int up(const double* h, size_t n, double** d) {

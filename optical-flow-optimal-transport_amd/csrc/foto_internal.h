@@ -38,6 +38,7 @@ void set_error(const char* fmt, ...);
 // takes back a stream with no work pending (callers synchronise first).  Never destroyed.
 int stream_acquire(hipStream_t* out);
 void stream_release(hipStream_t s);
+int stream_device(hipStream_t s);   // the device a pooled stream belongs to (-1: not pooled)
 
 // ----------------------------------------------------------------------------- geometry
 // One time-slab shard of the (Nt, Ny, Nx) grid: local planes l in [0, nloc) are global
@@ -81,7 +82,7 @@ struct RedBuf {
 struct KTimer {
     bool on = false;
     std::vector<hipEvent_t> pool;
-    struct Pend { hipEvent_t a, b; int cls; double bytes; };
+    struct Pend { hipEvent_t a, b; int cls; double bytes; size_t id; };
     std::vector<Pend> pend;
     int64_t n[8] = {0};
     double ms[8] = {0};
@@ -105,7 +106,7 @@ struct KTimer {
         hipEvent_t b = get();
         if (!b) return;
         (void)hipEventRecord(b, s);
-        pend.push_back({a, b, cls, by});
+        pend.push_back({a, b, cls, by, next_id++});
     }
     // drop the `count` most recent pending records of class cls (launches that turned out to
     // be no-ops, e.g. s-step passes enqueued after the solve had finished)
@@ -118,8 +119,25 @@ struct KTimer {
             --count;
         }
     }
-    size_t pending() const { return pend.size(); }
-    // the first n pending intervals (all complete: recorded before the last stream sync)
+    // marks are record ids (records are pushed in id order; ids survive discard_last)
+    size_t next_id = 0;
+    size_t mark() const { return next_id; }
+    size_t count_before(size_t m) const {
+        size_t n = 0;
+        while (n < pend.size() && pend[n].id < m) ++n;
+        return n;
+    }
+    // drop every record from mark m on (launches of an outer iteration that was rolled back)
+    void discard_from(size_t m) {
+        const size_t keep = count_before(m);
+        for (size_t k = keep; k < pend.size(); ++k) {
+            pool.push_back(pend[k].a);
+            pool.push_back(pend[k].b);
+        }
+        pend.resize(keep);
+    }
+    // the pending intervals before mark m (all complete: recorded before the last stream sync)
+    void resolve_upto(size_t m) { resolve_first(count_before(m)); }
     void resolve_first(size_t n) {
         n = std::min(n, pend.size());
         for (size_t k = 0; k < n; ++k) {

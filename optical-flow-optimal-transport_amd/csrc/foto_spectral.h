@@ -16,10 +16,17 @@ struct SpectralPlan {
     // travels to a pinned copy behind them.  done_flag() is the device flag a consumer can
     // guard on.  After the caller's stream sync, finish() reports the result; if the passes
     // did not suffice (*redo = 1) it runs the rest of the solve, polling, and recomputes x.
+    // The Gauss CG takes up to two deferred solves in flight (two outer iterations on the
+    // stream, foto_bb.cpp): finish() completes the oldest; a failed oldest solve (see
+    // oldest_needs_redo) is redone only after the newer one has been dropped (drop_newest,
+    // after a stream sync) -- its done flag chain kept that one's consumer from running.
     bool deferrable() const;
     int solve_deferred(double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s);
     const int* done_flag() const;
     int finish(int* iters, int* info, int* redo, KTimer* kt, hipStream_t s);
+    int pending() const;
+    bool oldest_needs_redo() const;   // after the stream has passed the oldest solve's header copy
+    int drop_newest(hipStream_t s);
 
     // ---- sharded phases (driven by foto_bb.cpp, all-to-all / all-gather in between)
     int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, pack -> stage

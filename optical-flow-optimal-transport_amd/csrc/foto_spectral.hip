@@ -15,6 +15,7 @@
 // (v_mfma_f64_16x16x4_f64), 64x64x16 block tiles staged through LDS.
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -2772,11 +2773,15 @@ struct SpecImpl {
     bool tcol = false;            // single shard, s-step, Nt in FOTO_TCOL_SIZES
     int tcol_nb = 0;              // column kernels' blocks
     int last_passes = 0;          // passes of the previous s-step solve (first chunk size)
-    // deferred solve in flight (solve_deferred -> finish)
-    bool pending = false;
-    int pend_launched = 0, pend_maxiter = 0;
-    double pend_rtol = 0.0;
-    double *pend_b = nullptr, *pend_x = nullptr;
+    // deferred solves in flight (solve_deferred -> finish), oldest first: one for the s-step
+    // CG, up to two for the Gauss CG (two outer iterations in flight)
+    struct Pend {
+        int launched = 0, maxiter = 0, hslot = 0;
+        double rtol = 0.0;
+        double *b = nullptr, *x = nullptr;
+    };
+    Pend pq[2];
+    int npend = 0;
     int sstep = 1;
     bool split_plan = false;
     std::vector<void*> allocs;
@@ -2785,7 +2790,8 @@ struct SpecImpl {
     // Gauss-compressed CG (cg_mode 3, foto_gauss.inc); gauss_active: the solve in flight uses it
     bool gauss = false, gauss_active = false;
     GqState* gq = nullptr;
-    GqState* hgq = nullptr;       // pinned: the header (K, status, conv, done, bn2, rn2)
+    GqState* hgq2[2] = {nullptr, nullptr};   // pinned: the header (K, status, conv, done, bn2, rn2) of
+    int hslot = 0, hlast = 0;                // the last two solves (hslot: the next one's)
     GqNodes* gqn = nullptr;
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
     double* gq_tab = nullptr;
@@ -2812,7 +2818,8 @@ struct SpecImpl {
         for (void* p : allocs) (void)hipFree(p);
         if (hS) (void)hipHostFree(hS);
         if (hS2) (void)hipHostFree(hS2);
-        if (hgq) (void)hipHostFree(hgq);
+        for (GqState* h : hgq2)
+            if (h) (void)hipHostFree(h);
     }
     SpecTab tab() const {
         SpecTab T;
@@ -3011,7 +3018,10 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     if (P->gauss) {
         FOTO_TRY(P->alloc(sizeof(GqState), &b)); P->gq = (GqState*)b;
         FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
-        FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq, sizeof(GqState)));
+        for (GqState*& h : P->hgq2) {
+            FOTO_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(GqState)));
+            std::memset((void*)h, 0, sizeof(GqState));
+        }
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
         FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
@@ -3357,51 +3367,70 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->gq_exact, P->world, P->r * P->eps, P->c1, P->gqn);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, P->gq);
+    const char* kl = getenv("FOTO_GQ_KLIM");   // (tests: force the s-step redo path)
+    const int klim = kl ? std::max(0, std::min(GQ_KMAX, atoi(kl))) : GQ_KMAX;
+    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq);
     FOTO_HIP_CHECK(hipGetLastError());
     k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->r * P->eps, P->c1, P->gq_tab);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq, P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
+    P->hlast = P->hslot;
+    P->hslot ^= 1;
+    FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq2[P->hlast], P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
     P->gauss_active = true;
     return 0;
 }
 
+// a failed solve broke the done chain (k_gq_cg); once it is redone, later solves may run again
+static int gq_unbreak(SpecImpl* P, hipStream_t s) {
+    FOTO_HIP_CHECK(hipMemsetAsync(&P->gq->broken, 0, sizeof(int), s));
+    return 0;
+}
 
-// single shard: b (physical, clobbered) -> b^ -> measure -> CG -> x, all enqueued
-static int gq_enqueue(SpecImpl* P, double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
+
+// single shard: b (physical) -> b^ -> measure -> CG -> x, all enqueued.  b is only read: the
+// transforms run through the box buffers (b -x-> tmp -y-> rh -t-> b^; x^ -> rh / tmp ... -> x),
+// so F survives a solve whose prox was skipped -- a failed solve with the next outer iteration
+// already enqueued behind it (foto_bb.cpp) then finds its right-hand side intact.
+static int gq_enqueue(SpecImpl* P, const double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
-    if (P->tcol) {
-        hipEvent_t e = kt ? kt->start(s) : nullptr;
-        FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
-        FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, b, s));
-        FOTO_HIP_CHECK(launch_tcol(P, false, b, nullptr, rtol, maxiter, s, TC_PLAIN));
-        if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
-    } else {
-        FOTO_TRY(forward3(P, b, P->tmp, P->bh, kt, s));
-    }
+    hipEvent_t e = kt ? kt->start(s) : nullptr;
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, P->rh, s));
+    if (P->tcol) FOTO_HIP_CHECK(launch_tcol(P, false, P->rh, nullptr, rtol, maxiter, s, TC_PLAIN));
+    else FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, (int)g.nxy, P->rh, P->bh, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
     FOTO_TRY(gq_measure(P, kt, s));
     FOTO_TRY(gq_solve(P, rtol, maxiter, kt, s));
-    if (P->tcol) return tcol_inverse(P, b, x, rtol, maxiter, kt, s);   // launch_tcol: the Q kernel
-    FOTO_HIP_CHECK(gq_xhat(P, P->tmp, s));
-    return inverse3(P, P->tmp, b, x, kt, s);
+    e = kt ? kt->start(s) : nullptr;
+    if (P->tcol) {
+        FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, P->tmp, rtol, maxiter, s));   // x^ -> rh, t^-1 -> tmp
+    } else {
+        FOTO_HIP_CHECK(gq_xhat(P, P->rh, s));
+        FOTO_HIP_CHECK(dct_pass(P, 2, true, 1, (int)g.nxy, P->rh, P->tmp, s));
+    }
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, P->tmp, P->rh, s));
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.Nt * g.Ny, 1, P->rh, x, s));
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 7.0 * 8.0 * N);
+    return 0;
 }
 
 // the s-step CG from b^ (still intact) when the tables could not represent the solve
 static int gq_redo(SpecImpl* P, double* b, double* x, double rtol, int maxiter, int* iters, int* info, KTimer* kt,
                    hipStream_t s) {
     P->gauss_active = false;
+    FOTO_TRY(gq_unbreak(P, s));
     FOTO_TRY(solve_s2(P, rtol, maxiter, 0, iters, info, kt, s, false));
     if (P->tcol) return tcol_inverse(P, b, x, rtol, maxiter, kt, s);
     FOTO_HIP_CHECK(launch_xhat(P, s));
     return inverse3(P, P->tmp, b, x, kt, s);
 }
 
-// after the stream has passed gq_solve's header copy
-static void gq_result(const SpecImpl* P, int maxiter, int* iters, int* info) {
-    *iters = P->hgq->K;
-    *info = P->hgq->conv ? 0 : maxiter;
+// after the stream has passed the header copy of the solve in ring slot h
+static void gq_result(const SpecImpl* P, int h, int maxiter, int* iters, int* info) {
+    *iters = P->hgq2[h]->K;
+    *info = P->hgq2[h]->conv ? 0 : maxiter;
 }
 
 // single shard, s-step, column-kernel t axis: b -x-> tmp -y-> b -t(+INIT)-> b^; CG passes;
@@ -3423,8 +3452,8 @@ static int solve_tcol(SpecImpl* P, double* b, double* x, double rtol, int maxite
 
 bool SpectralPlan::deferrable() const {
     const SpecImpl* P = (const SpecImpl*)impl;
-    if (P->gauss) return P->world == 1;   // fixed work: nothing to predict
-    return P->tcol && P->sstep == 2 && P->world == 1 && P->last_passes > 0;
+    if (P->gauss) return P->world == 1 && P->npend < 2;   // fixed work: nothing to predict
+    return P->tcol && P->sstep == 2 && P->world == 1 && P->last_passes > 0 && P->npend == 0;
 }
 
 const int* SpectralPlan::done_flag() const {
@@ -3432,19 +3461,24 @@ const int* SpectralPlan::done_flag() const {
     return P->gauss ? &P->gq->done : &P->S2->done;
 }
 
+int SpectralPlan::pending() const { return ((const SpecImpl*)impl)->npend; }
+
 int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
-    if (!deferrable() || P->pending) {
-        set_error("spectral CG: deferred solve needs a single-shard s-step plan after a finished solve");
+    if (!deferrable()) {
+        set_error("spectral CG: deferred solve needs a single-shard plan with a free slot (s-step: after a finished solve)");
         return FOTO_ERR_STATE;
     }
+    SpecImpl::Pend& d = P->pq[P->npend];
+    d.b = b;
+    d.x = x;
+    d.rtol = rtol;
+    d.maxiter = maxiter;
+    d.launched = 0;
     if (P->gauss) {
         FOTO_TRY(gq_enqueue(P, b, x, rtol, maxiter, kt, s));
-        P->pending = true;
-        P->pend_b = b;
-        P->pend_x = x;
-        P->pend_rtol = rtol;
-        P->pend_maxiter = maxiter;
+        d.hslot = P->hlast;
+        ++P->npend;
         return 0;
     }
     const Geo& g = P->g;
@@ -3466,53 +3500,73 @@ int SpectralPlan::solve_deferred(double* b, double* x, double rtol, int maxiter,
     }
     FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
     FOTO_TRY(tcol_inverse(P, b, x, rtol, maxiter, kt, s));
-    P->pending = true;
-    P->pend_launched = n;
-    P->pend_b = b;
-    P->pend_x = x;
-    P->pend_rtol = rtol;
-    P->pend_maxiter = maxiter;
+    d.launched = n;
+    ++P->npend;
     return 0;
+}
+
+bool SpectralPlan::oldest_needs_redo() const {
+    const SpecImpl* P = (const SpecImpl*)impl;
+    if (P->npend == 0) return false;
+    if (P->gauss) return P->hgq2[P->pq[0].hslot]->status != 0;
+    return !P->hS2->done;
+}
+
+int SpectralPlan::drop_newest(hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    if (P->npend == 0 || !P->gauss) {
+        set_error("spectral CG: no Gauss solve in flight to drop");
+        return FOTO_ERR_STATE;
+    }
+    --P->npend;
+    // the dropped solve may have failed or followed a failed one: its flags mean nothing now
+    return gq_unbreak(P, s);
 }
 
 int SpectralPlan::finish(int* iters, int* info, int* redo, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
-    if (!P->pending) {
+    if (P->npend == 0) {
         set_error("spectral CG: no deferred solve to finish");
         return FOTO_ERR_STATE;
     }
-    P->pending = false;
+    const SpecImpl::Pend d = P->pq[0];
+    P->pq[0] = P->pq[1];
+    --P->npend;
     *redo = 0;
     if (P->gauss) {
-        if (P->hgq->status != 0) {   // K beyond the table or a breakdown: the s-step CG from b^
+        if (P->hgq2[d.hslot]->status != 0) {   // K beyond the table or a breakdown: the s-step CG from b^
+            if (P->npend != 0) {
+                set_error("spectral CG: a failed solve must be redone before the next one runs (drop it first)");
+                return FOTO_ERR_STATE;
+            }
             *redo = 1;
-            return gq_redo(P, P->pend_b, P->pend_x, P->pend_rtol, P->pend_maxiter, iters, info, kt, s);
+            return gq_redo(P, d.b, d.x, d.rtol, d.maxiter, iters, info, kt, s);
         }
-        gq_result(P, P->pend_maxiter, iters, info);
-        P->gauss_active = false;
+        gq_result(P, d.hslot, d.maxiter, iters, info);
+        if (P->npend == 0) P->gauss_active = false;
         return 0;
     }
-    int passes = P->pend_launched;
+    int passes = d.launched;
     if (!P->hS2->done) {   // the predicted passes were not enough: continue, polling, and redo x
         *redo = 1;
         const double N = P->nbox();
         while (!P->hS2->done) {
             for (int j = 0; j < 2; ++j, ++passes) {
                 hipEvent_t e = kt ? kt->start(s) : nullptr;
-                FOTO_HIP_CHECK(launch_s2(P, false, P->pend_rtol, P->pend_maxiter, nullptr, s));
+                FOTO_HIP_CHECK(launch_s2(P, false, d.rtol, d.maxiter, nullptr, s));
                 if (kt) kt->stop(e, s, FOTO_K_SPEC, 32.0 * N);
             }
             FOTO_HIP_CHECK(hipMemcpyAsync(P->hS2, P->S2, sizeof(SStep), hipMemcpyDeviceToHost, s));
             FOTO_HIP_CHECK(hipStreamSynchronize(s));
-            if (passes > P->pend_maxiter + 4) {
+            if (passes > d.maxiter + 4) {
                 set_error("spectral s-step CG did not terminate");
                 return FOTO_ERR_STATE;
             }
         }
-        FOTO_TRY(tcol_inverse(P, P->pend_b, P->pend_x, P->pend_rtol, P->pend_maxiter, kt, s));
+        FOTO_TRY(tcol_inverse(P, d.b, d.x, d.rtol, d.maxiter, kt, s));
     }
     *iters = P->hS2->iters;
-    *info = (P->hS2->done == 1) ? 0 : P->pend_maxiter;
+    *info = (P->hS2->done == 1) ? 0 : d.maxiter;
     P->last_passes = P->hS2->passes;
     if (kt) kt->discard_last(FOTO_K_SPEC, std::max(0, passes - P->hS2->passes));
     return 0;
@@ -3528,8 +3582,8 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
     if (P->gauss) {
         FOTO_TRY(gq_enqueue(P, b, x, rtol, maxiter, kt, s));
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
-        if (P->hgq->status != 0) return gq_redo(P, b, x, rtol, maxiter, iters, info, kt, s);
-        gq_result(P, maxiter, iters, info);
+        if (P->hgq2[P->hlast]->status != 0) return gq_redo(P, b, x, rtol, maxiter, iters, info, kt, s);
+        gq_result(P, P->hlast, maxiter, iters, info);
         P->gauss_active = false;
         return 0;
     }
@@ -3683,9 +3737,12 @@ int SpectralPlan::gauss_solve(double rtol, int maxiter, KTimer* kt, hipStream_t 
 int SpectralPlan::gauss_wait(int maxiter, int* ok, int* iters, int* info, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     FOTO_HIP_CHECK(hipStreamSynchronize(s));
-    *ok = P->hgq->status == 0;
-    gq_result(P, maxiter, iters, info);
-    if (!*ok) P->gauss_active = false;
+    *ok = P->hgq2[P->hlast]->status == 0;
+    gq_result(P, P->hlast, maxiter, iters, info);
+    if (!*ok) {
+        P->gauss_active = false;
+        FOTO_TRY(gq_unbreak(P, s));   // the s-step CG redoes this solve (foto_bb.cpp)
+    }
     return 0;
 }
 
@@ -3693,10 +3750,9 @@ void SpectralPlan::gauss_end() { ((SpecImpl*)impl)->gauss_active = false; }
 
 int SpectralPlan::reset(hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
-    P->pending = false;
+    P->npend = 0;
     P->gauss_active = false;
     if (P->gq) FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
-    P->pend_launched = 0;
     P->last_passes = 0;
     FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->rb.ticket, 0, 8 * sizeof(double), s));

@@ -5,7 +5,7 @@ sharding) through a C ABI (include/foto.h).  No PyTorch on the product path.
 """
 from ._lib import FotoError, lib, device_count  # noqa: F401
 from . import ops, bb, gn, synthetic  # noqa: F401
-from .bb import BBSolver, solve, CG_STENCIL, CG_SPECTRAL, CG_SSTEP  # noqa: F401
+from .bb import BBSolver, solve, CG_STENCIL, CG_SPECTRAL, CG_SSTEP, CG_GAUSS  # noqa: F401
 
 __all__ = ["FotoError", "lib", "device_count", "ops", "bb", "gn", "synthetic", "BBSolver", "solve",
-           "CG_STENCIL", "CG_SPECTRAL", "CG_SSTEP"]
+           "CG_STENCIL", "CG_SPECTRAL", "CG_SSTEP", "CG_GAUSS"]

@@ -41,7 +41,7 @@ def build_parser():
     p.add_argument("--lambdaa", nargs="?", type=float, default=0.2, help="Horn-Schunck lambda")
     # additions
     p.add_argument("--device", type=int, default=-1, help="HIP device ordinal (default: current)")
-    p.add_argument("--cg-mode", type=int, default=None, help="0 stencil, 1 spectral, 2 spectral s-step CG")
+    p.add_argument("--cg-mode", type=int, default=None, help="0 stencil, 1 spectral, 2 spectral s-step, 3 Gauss-compressed spectral CG (default)")
     return p
 
 

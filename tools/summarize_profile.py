@@ -41,6 +41,9 @@ LOAD_WIDTH = {"spec_cg": 16, "spec_cg1": 16, "spec_init": 16, "spec_xhat": 16, "
               "prox_sep": 8, "gq_hist": 16, "dct_t_q": 8, "dct_tp_q": 8, "dct_tp_init": 8, "dct_tp_xhat": 8,
               "rhs": 8, "dct_fft_fwd": 8, "dct_fft_inv": 8, "dct_t_init": 8, "dct_t_xhat": 8, "dct_gemm": 8, "flow": 8,
               "gn_dir": 8, "gn_upd": 8}
+# kernels of one outer iteration of the default path (profiles' "_step" traffic)
+STEP_KERNELS = {"dct_fft_fwd", "dct_fft_inv", "dct_t_init", "dct_t_xhat", "dct_tp_init", "dct_tp_xhat", "dct_gemm",
+                "gq_hist", "gq_reduce", "gq_nodes", "gq_cg", "gq_qtab", "gq_xhat", "prox"}
 CALIB_BYTES = {"rd8": 2 << 30, "rd16": 2 << 30, "wr8": 1 << 30, "wr16": 1 << 30}
 
 
@@ -152,7 +155,19 @@ def main():
         # bench run itself)
         src = {"_source": f"profiles/{a.tag}_rocprof_summary.md (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, "
                           f"calibrated by tools/calib_fetch)"}
-        json.dump({**src, **traffic}, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
+        out = {**src, **traffic}
+        # the whole outer iteration (mode 3, one GPU): every kernel launched per outer iteration,
+        # summed over the profiled run and divided by the outer iterations (one prox each)
+        step_k = [k for k in traffic if k in STEP_KERNELS]
+        if "prox" in traffic and traffic["prox"]["launches"] > 0:
+            n_outer = traffic["prox"]["launches"]
+            tot = sum(traffic[k]["hbm_bytes_per_launch"] * traffic[k]["launches"] for k in step_k)
+            out["_step"] = {"hbm_bytes_per_step": tot / n_outer, "outer_iterations": n_outer, "kernels": step_k,
+                            "source": src["_source"]}
+            lines += ["", f"## HBM traffic per outer iteration: {tot / n_outer / 1e6:.1f} MB "
+                          f"({n_outer} outer iterations; kernels {', '.join(step_k)})"]
+            open(os.path.join(a.out, f"{a.tag}_rocprof_summary.md"), "w").write("\n".join(lines) + "\n")
+        json.dump(out, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
 
 
