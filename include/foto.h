@@ -164,6 +164,7 @@ int foto_nccl_unique_id(void* out128);
 #define FOTO_XFER_BOX_TO_SLAB 2   /* spectral all-to-all: row boxes -> time slabs             */
 #define FOTO_XFER_RELAY 3         /* trajectory positions rank j -> j + 1 (flow extraction)   */
 #define FOTO_XFER_DELIVER 4       /* (u, v, m) last rank -> rank 0                            */
+#define FOTO_XFER_HALO2 5         /* two halo planes per side (phi of the fused prox + RHS)   */
 #define FOTO_CALL_SEND 0
 #define FOTO_CALL_RECV 1
 #define FOTO_CALL_COPY 2

@@ -94,8 +94,11 @@ struct Shard {
     double* q[3] = {nullptr, nullptr, nullptr};
     double* nu[3] = {nullptr, nullptr, nullptr};   // second mu buffer of the fused prox + RHS
     double* xi[3] = {nullptr, nullptr, nullptr};   // third mu buffer (two outer iterations in flight)
-    double* phi = nullptr;   // CG iterate x
+    double* phi = nullptr;   // CG iterate x (two halo planes per side: the fused prox reads them)
     double* phi_alt = nullptr;   // the other phi of the pipelined loop
+    // the last fused prox + RHS launch's mu in / out (fz_src is the mu stepB of phi used)
+    double* fz_src[3] = {nullptr, nullptr, nullptr};
+    double* fz_dst[3] = {nullptr, nullptr, nullptr};
     double* rv = nullptr;    // CG residual (starts as F)
     double* p[2] = {nullptr, nullptr};
     double* rho0 = nullptr;
@@ -120,14 +123,15 @@ struct Shard {
         allocs.push_back(*out);
         return 0;
     }
-    // (nloc + 2) planes, zeroed on the context's stream: a hipMemset (null stream) is not
-    // ordered with the non-blocking stream the kernels run on -- it raced with k_init_mu
-    int alloc_field(double** out, hipStream_t st) {
+    // (nloc + 2 h) planes (h halo planes per side), zeroed on the context's stream: a hipMemset
+    // (null stream) is not ordered with the non-blocking stream the kernels run on -- it raced
+    // with k_init_mu
+    int alloc_field(double** out, hipStream_t st, int h = 1) {
         void* b = nullptr;
-        const size_t n = (size_t)(g.nloc + 2) * (size_t)g.nxy;
+        const size_t n = (size_t)(g.nloc + 2 * h) * (size_t)g.nxy;
         FOTO_TRY(alloc(n * sizeof(double), &b));
         FOTO_HIP_CHECK(hipMemsetAsync(b, 0, n * sizeof(double), st));
-        *out = (double*)b + g.nxy;
+        *out = (double*)b + (size_t)h * g.nxy;
         return 0;
     }
     ~Shard() {
@@ -154,12 +158,10 @@ struct foto_bb_ctx {
     int last_cg = 0;
     int last_passes = 0;   // s-step passes of the previous sharded spectral solve
     int have_phi = 0;
-    // single shard: prox fused with the next RHS (k_prox_rhs); F in rv is then produced by
-    // the previous outer iteration (f_ready), mu rotates through Shard::mu / nu (/ xi)
+    // prox fused with the next RHS (k_prox_rhs); F in rv is then produced by the previous
+    // outer iteration (f_ready), mu rotates through Shard::mu / nu (/ xi)
     bool fuse = false;
     bool f_ready = false;
-    double* fz_src[3] = {nullptr, nullptr, nullptr};   // the last fused launch's mu in / out
-    double* fz_dst[3] = {nullptr, nullptr, nullptr};
     // Two outer iterations in flight (single shard, fused, Gauss CG; FOTO_PIPE=0: one): the
     // host enqueues iteration i + 1 before it waits for iteration i's crit, so the GPU never
     // idles while the host wakes up and launches.  mu rotates through three buffers and phi
@@ -291,9 +293,9 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     const int nlocal = c->rccl ? 1 : W;
     {
         const char* e = getenv("FOTO_FUSE_PR");   // 0: separate k_prox / k_rhs (A/B runs)
-        c->fuse = (W == 1) && !(e && atoi(e) == 0);
+        c->fuse = !(e && atoi(e) == 0);
         const char* pe = getenv("FOTO_PIPE");   // 0: one outer iteration in flight (A/B runs)
-        c->pipe = c->fuse && c->o.cg_mode == 3 && !(pe && atoi(pe) == 0);
+        c->pipe = W == 1 && c->fuse && c->o.cg_mode == 3 && !(pe && atoi(pe) == 0);
     }
     for (int j = 0; j < nlocal; ++j) {
         auto sp = std::make_unique<Shard>();
@@ -309,9 +311,9 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
             for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.nu[f], c->s));
         if (c->pipe) {
             for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.xi[f], c->s));
-            FOTO_TRY(s.alloc_field(&s.phi_alt, c->s));
+            FOTO_TRY(s.alloc_field(&s.phi_alt, c->s, 2));
         }
-        FOTO_TRY(s.alloc_field(&s.phi, c->s));
+        FOTO_TRY(s.alloc_field(&s.phi, c->s, 2));
         FOTO_TRY(s.alloc_field(&s.rv, c->s));
         FOTO_TRY(s.alloc_field(&s.p[0], c->s));
         FOTO_TRY(s.alloc_field(&s.p[1], c->s));
@@ -533,15 +535,26 @@ static int outer_head(foto_bb_ctx* c) {
     return 0;
 }
 
-// the fused k_prox_rhs on the pair recorded in fz_src -> fz_dst (single shard)
+// the fused k_prox_rhs of every local shard on the pair recorded in its fz_src -> fz_dst;
+// sharded: the two-plane phi halo and the one-plane halo of the mu it reads go first
 static int prox_rhs(foto_bb_ctx* c, const int* guard) {
-    Shard& s = *c->sh[0];
-    const double nv = (double)s.g.nloc * (double)s.g.nxy;
-    hipEvent_t e = c->kt.start(c->s);
-    FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], c->fz_dst[0], c->fz_dst[1],
-                                   c->fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(1),
-                                   c->o.cg_mode == 0 ? s.gath_rr() : nullptr, c->s, guard));
-    c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
+    const int W = c->W;
+    if (W > 1) {
+        FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
+                          [](Shard& s) { return s.phi; }));
+        for (int f = 0; f < 3; ++f) FOTO_TRY(halo(c, [f](Shard& s) { return s.fz_src[f]; }));
+    }
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        hipEvent_t e = c->kt.start(c->s);
+        FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.fz_dst[0], s.fz_dst[1],
+                                       s.fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(W) + 2 * s.rank,
+                                       c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s, guard));
+        c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
+    }
+    // the stencil CG's F.F (its stopping rule) from every rank
+    if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
     return 0;
 }
 
@@ -554,7 +567,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     e.kmark = kmark;
     for (int f = 0; f < 3; ++f) {
         e.mu[f] = s0.mu[f]; e.nu[f] = s0.nu[f]; e.xi[f] = s0.xi[f];
-        e.fz_src[f] = c->fz_src[f]; e.fz_dst[f] = c->fz_dst[f];
+        e.fz_src[f] = s0.fz_src[f]; e.fz_dst[f] = s0.fz_dst[f];
     }
     e.phi = s0.phi;
     e.phi_alt = s0.phi_alt;
@@ -589,18 +602,20 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     if (c->fuse) {
         // prox + the next iteration's RHS: mu -> nu, F -> rv; then nu is the current mu
         // (pipelined: mu -> nu -> xi -> mu rotate, so the mu before this iteration survives it)
-        for (int f = 0; f < 3; ++f) { c->fz_src[f] = s0.mu[f]; c->fz_dst[f] = s0.nu[f]; }
+        for (auto& sp : c->sh)
+            for (int f = 0; f < 3; ++f) { sp->fz_src[f] = sp->mu[f]; sp->fz_dst[f] = sp->nu[f]; }
         FOTO_TRY(prox_rhs(c, dsp ? dsp->done_flag() : nullptr));
-        for (int f = 0; f < 3; ++f) {
-            if (c->pipe) {
-                double* m = s0.mu[f];
-                s0.mu[f] = s0.nu[f];
-                s0.nu[f] = s0.xi[f];
-                s0.xi[f] = m;
-            } else {
-                std::swap(s0.mu[f], s0.nu[f]);
+        for (auto& sp : c->sh)
+            for (int f = 0; f < 3; ++f) {
+                if (c->pipe) {
+                    double* m = sp->mu[f];
+                    sp->mu[f] = sp->nu[f];
+                    sp->nu[f] = sp->xi[f];
+                    sp->xi[f] = m;
+                } else {
+                    std::swap(sp->mu[f], sp->nu[f]);
+                }
             }
-        }
         c->f_ready = true;
     } else {
         FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
@@ -635,14 +650,14 @@ static int rollback(foto_bb_ctx* c) {
     c->kt.discard_from(e.kmark);
     for (int f = 0; f < 3; ++f) {
         s0.mu[f] = e.mu[f]; s0.nu[f] = e.nu[f]; s0.xi[f] = e.xi[f];
-        c->fz_src[f] = e.fz_src[f]; c->fz_dst[f] = e.fz_dst[f];
+        s0.fz_src[f] = e.fz_src[f]; s0.fz_dst[f] = e.fz_dst[f];
     }
     s0.phi = e.phi;
     s0.phi_alt = e.phi_alt;
     c->hpar = e.hpar;
-    if (e.f_ready && c->fz_src[0]) {
+    if (e.f_ready && s0.fz_src[0]) {
         // q of the kept iteration (stepB of its phi and the mu before it), for the next head's RHS
-        FOTO_HIP_CHECK(launch_q_from_phi(s0.g, s0.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], s0.q[0], s0.q[1],
+        FOTO_HIP_CHECK(launch_q_from_phi(s0.g, s0.phi, s0.fz_src[0], s0.fz_src[1], s0.fz_src[2], s0.q[0], s0.q[1],
                                          s0.q[2], c->r, c->s));
     }
     c->f_ready = false;   // (a dropped first iteration leaves mu, q as they were: the head recomputes F)
@@ -801,6 +816,7 @@ int foto_xfer_calls(int kind, int Nt, int Ny, int Nx, int world, int rank, int a
             xs = relay_xfers(nxy, arg);
             break;
         case FOTO_XFER_DELIVER: xs = deliver_xfers(nxy, world); break;
+        case FOTO_XFER_HALO2: xs = halo_depth_xfers(Nt, nxy, world, 2); break;
         default: set_error("foto_xfer_calls: unknown kind %d", kind); return FOTO_ERR_ARG;
     }
     const std::vector<Call> cs = rccl_calls(xs, rank);
@@ -940,9 +956,11 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         Shard& s = *sp;
         const size_t bytes = (size_t)(s.g.nloc + 2) * (size_t)nxy * sizeof(double);
         double* fields[] = {s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], s.nu[0], s.nu[1], s.nu[2],
-                            s.xi[0], s.xi[1], s.xi[2], s.phi, s.phi_alt, s.rv, s.p[0], s.p[1]};
+                            s.xi[0], s.xi[1], s.xi[2], s.rv, s.p[0], s.p[1]};
         for (double* f : fields)   // as ctx_init leaves them: zero, halo planes included
             if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - nxy, 0, bytes, c->s));
+        for (double* f : {s.phi, s.phi_alt})   // (two halo planes per side)
+            if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - 2 * nxy, 0, bytes + 2 * nxy * sizeof(double), c->s));
         FOTO_HIP_CHECK(hipMemsetAsync(s.gath, 0, sizeof(double) * 4 * c->W, c->s));
         FOTO_HIP_CHECK(hipMemsetAsync(s.rb.ticket, 0, sizeof(unsigned) * 64, c->s));
         FOTO_HIP_CHECK(hipMemsetAsync(s.S, 0, sizeof(CGScal), c->s));
@@ -955,7 +973,8 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     c->last_passes = 0;
     c->have_phi = 0;
     c->f_ready = false;
-    for (int f = 0; f < 3; ++f) c->fz_src[f] = c->fz_dst[f] = nullptr;
+    for (auto& sp : c->sh)
+        for (int f = 0; f < 3; ++f) sp->fz_src[f] = sp->fz_dst[f] = nullptr;
     c->prev_crit = -1;
     c->st = foto_bb_stats{};
     c->kt.resolve();
@@ -992,9 +1011,12 @@ int foto_bb_get_phi(foto_bb_ctx* c, double* phi) {
 int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3) {
     if (!c) return FOTO_ERR_ARG;
     if (q3 && c->fuse && c->have_phi) {   // the fused kernel never stores q: recompute it (bit-identical)
-        Shard& s = *c->sh[0];
-        FOTO_HIP_CHECK(launch_q_from_phi(s.g, s.phi, c->fz_src[0], c->fz_src[1], c->fz_src[2], s.q[0], s.q[1],
-                                         s.q[2], c->r, c->s));
+        for (auto& sp : c->sh) {   // (phi's halo planes are the ones the last prox read)
+            Shard& s = *sp;
+            if (!s.fz_src[0]) continue;
+            FOTO_HIP_CHECK(launch_q_from_phi(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.q[0], s.q[1],
+                                             s.q[2], c->r, c->s));
+        }
     }
     size_t tot = 0;
     for (auto& sp : c->sh) tot += (size_t)sp->g.nloc * sp->g.nxy;

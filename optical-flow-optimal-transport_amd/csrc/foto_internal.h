@@ -214,8 +214,10 @@ hipError_t launch_cg_upd(const Geo& g, int k, const double* p, double* x, double
 hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux, double* muy, double* qt,
                        double* qx, double* qy, double r, RedBuf rb, double* gath, int rank, hipStream_t s,
                        const int* guard = nullptr);
-// single shard: k_prox fused with the next iteration's RHS (mu -> nu, F, crit num/den ->
-// gath_crit[0..1], F.F -> gath_rr[0] when non-null); needs rb.cap >= 3 * prox_rhs_blocks(g)
+// k_prox fused with the next iteration's RHS (mu -> nu, F, this rank's crit num/den ->
+// gath_crit[0..1], F.F -> gath_rr[0] when non-null); needs rb.cap >= 3 * prox_rhs_blocks(g).
+// Sharded (g.t0 > 0 or g.t0 + g.nloc < g.Nt): phi needs two valid halo planes on each side
+// and mu one (the neighbours' boundary planes), exchanged before the launch.
 int prox_rhs_blocks(const Geo& g);
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,

@@ -711,10 +711,13 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 // a one-voxel ring (66 x 10: the x / y neighbours F needs) and on the planes l0 - 1 and l1
 // (the t neighbours), which needs phi on a two-voxel ring (68 x 12) and planes l0 - 2 .. l1 + 1.
 // mu' goes to a second buffer (neighbouring blocks still read the old mu of their ring voxels).
-// Single shard only (the sharded path exchanges halo planes between the two halves).
-// Per voxel the arithmetic is k_prox's and k_rhs's, in the same order: mu', F and the crit
-// terms are bit-identical to the unfused kernels; only the crit / F.F sums are grouped
-// differently.
+// Time-sharded, a shard's first and last chunks recompute stepB on the neighbouring ranks'
+// boundary planes exactly as the chunk seams do: phi carries two halo planes and mu one on
+// each side (exchanged before the launch), so a rank's F needs nothing after its own launch.
+// Plane indices p are local (memory: p * nxy, p in [-2, nloc + 1]); t = t0 + p is global
+// (boundary conditions).  Per voxel the arithmetic is k_prox's and k_rhs's, in the same order:
+// mu', F and the crit terms are bit-identical to the unfused kernels; only the crit / F.F sums
+// are grouped differently.
 //
 // Iteration p of the march (p = max(l0 - 1, 0) .. l1): store phi(p + 2) (loaded during the
 // previous iteration) into a 4-plane LDS ring, issue the loads of phi(p + 3) and mu(p + 1),
@@ -747,12 +750,12 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     if (guard && *guard == 0) return;
     __shared__ double fr[4][PR_FN];                  // phi ring (plane p in slot p & 3)
     __shared__ double wb[2][2][PR_PH * PR_PW];       // [plane & 1][x | y part] of w
-    const int Nt = g.Nt, Nx = g.Nx, Ny = g.Ny;
+    const int Nt = g.Nt, Nx = g.Nx, Ny = g.Ny, t0 = g.t0;
     const int64_t nxy = g.nxy;
     const int ntx = (Nx + PR_X - 1) / PR_X, ntiles = ntx * ((Ny + PR_Y - 1) / PR_Y);
     const int lin = xcd_tile(blockIdx.x);
     const int ch = lin / ntiles, tile = lin - ch * ntiles;
-    const int l0 = ch * tch, l1 = min(Nt, l0 + tch);
+    const int l0 = ch * tch, l1 = min(g.nloc, l0 + tch);   // own planes of this chunk (local)
     const int x0 = (tile % ntx) * PR_X, y0 = (tile / ntx) * PR_Y;
     const int tid = threadIdx.x;
     // own voxel: stepB region position (1 + tid % 64, 1 + tid / 64)
@@ -780,12 +783,13 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         fin[j] = idx < PR_FN && xx >= 0 && xx < Nx && yy >= 0 && yy < Ny;
         foff[j] = fin[j] ? yy * Nx + xx : 0;
     }
-    const int pa = max(l0 - 1, 0), pz = min(l1, Nt - 1);   // stepB planes
+    const int pa = max(l0 - 1, -t0), pz = min(l1, Nt - 1 - t0);   // stepB planes (local; >= -1, <= nloc)
     double fv[PR_FR];
     auto load_phi_to = [&](int p, double (&v)[PR_FR]) {   // planes beyond pz + 1 are never read
+        const bool ok = t0 + p >= 0 && p <= pz + 1 && t0 + p < Nt;
 #pragma unroll
         for (int j = 0; j < PR_FR; ++j)
-            v[j] = (p >= 0 && p <= pz + 1 && p < Nt && fin[j]) ? phi[p * nxy + foff[j]] : 0.0;
+            v[j] = (ok && fin[j]) ? phi[p * nxy + foff[j]] : 0.0;
     };
     auto store_phi_from = [&](int p, const double (&v)[PR_FR]) {
 #pragma unroll
@@ -801,13 +805,14 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         if (own) { om[0] = mut[p * nxy + ooff]; om[1] = mux[p * nxy + ooff]; om[2] = muy[p * nxy + ooff]; }
         if (hal) { hm[0] = mut[p * nxy + hoff]; hm[1] = mux[p * nxy + hoff]; hm[2] = muy[p * nxy + hoff]; }
     };
-    // stepB / stepC at stepB-region position (px, py) of plane t (k_prox's body)
-    auto stepb = [&](int t, int px, int py, int xg, int yg, const double (&m)[3], double (&w)[3], double& n0o,
+    // stepB / stepC at stepB-region position (px, py) of local plane p (k_prox's body)
+    auto stepb = [&](int p, int px, int py, int xg, int yg, const double (&m)[3], double (&w)[3], double& n0o,
                      double& ao, double& gto, double& gxo, double& gyo, double (&nu)[3]) {
+        const int t = t0 + p;
         const int fi = (py + 1) * PR_FW + px + 1;
-        const double* P = fr[t & 3];
+        const double* P = fr[p & 3];
         const double c = P[fi];
-        const double tm = t > 0 ? fr[(t - 1) & 3][fi] : 0.0, tp = t < Nt - 1 ? fr[(t + 1) & 3][fi] : 0.0;
+        const double tm = t > 0 ? fr[(p - 1) & 3][fi] : 0.0, tp = t < Nt - 1 ? fr[(p + 1) & 3][fi] : 0.0;
         const double gt = d1w(t, Nt, tm, c, tp);
         const double gx = d1w(xg, Nx, P[fi - 1], c, P[fi + 1]);
         const double gy = d1w(yg, Ny, P[fi - PR_FW], c, P[fi + PR_FW]);
@@ -878,19 +883,19 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         const double cm[3] = {om[0], om[1], om[2]}, chm[3] = {hm[0], hm[1], hm[2]};   // mu(p)
         load_mu(p + 1);
         if (p <= pz) plane(p, cm, chm);
-        else wtn = 0.0;   // p = Nt: F(Nt - 1) reads no w_t(Nt)
-        const int n = p - 1;
+        else wtn = 0.0;   // t0 + p = Nt: F(Nt - 1) reads no w_t(Nt)
+        const int n = p - 1, tn = t0 + n;
         if (own && n >= l0) {
             // F(n) (k_rhs's order: t, x, y terms, then the boundary-plane corrections)
             const double* WX = wb[n & 1][0];
             const double* WY = wb[n & 1][1];
             const int ci = opy * PR_PW + opx;
             double s = 0.0;
-            acc_d1w(s, n, Nt, wtm, wtc, wtn);
+            acc_d1w(s, tn, Nt, wtm, wtc, wtn);
             acc_d1w(s, ox, Nx, ox > 0 ? WX[ci - 1] : 0.0, WX[ci], ox < Nx - 1 ? WX[ci + 1] : 0.0);
             acc_d1w(s, oy, Ny, oy > 0 ? WY[ci - PR_PW] : 0.0, WY[ci], oy < Ny - 1 ? WY[ci + PR_PW] : 0.0);
-            if (n == 0) s -= (rho0[ooff] - bcm) + r * bcq;
-            if (n == Nt - 1) s += (rhoT[ooff] - bcm) + r * bcq;
+            if (tn == 0) s -= (rho0[ooff] - bcm) + r * bcq;
+            if (tn == Nt - 1) s += (rhoT[ooff] - bcm) + r * bcq;
             F[n * nxy + ooff] = s;
             ff += s * s;
         }
@@ -901,7 +906,7 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         __syncthreads();
     }
     double v[3] = {num, den, ff}, tot[3];
-    if (grid_reduce_last<3, PR_NT>(v, rb, tot) && threadIdx.x == 0) {
+    if (grid_reduce_last<3, PR_NT>(v, rb, tot) && threadIdx.x == 0) {   // (this rank's slots)
         gath_crit[0] = tot[0];
         gath_crit[1] = tot[1];
         if (gath_rr) gath_rr[0] = tot[2];
@@ -914,18 +919,17 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
 int prox_rhs_tch(const Geo& g) {
     const char* e = getenv("FOTO_PR_TCH");
     const int v = e ? atoi(e) : 16;
-    return std::min(v > 0 ? v : 16, g.Nt);
+    return std::min(v > 0 ? v : 16, g.nloc);
 }
 
 int prox_rhs_blocks(const Geo& g) {
     const int tch = prox_rhs_tch(g);
-    return ((g.Nx + PR_X - 1) / PR_X) * ((g.Ny + PR_Y - 1) / PR_Y) * ((g.Nt + tch - 1) / tch);
+    return ((g.Nx + PR_X - 1) / PR_X) * ((g.Ny + PR_Y - 1) / PR_Y) * ((g.nloc + tch - 1) / tch);
 }
 
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard) {
-    if (g.t0 != 0 || g.nloc != g.Nt) return hipErrorInvalidValue;   // single shard only
     const int nb = prox_rhs_blocks(g);
     if (rb.cap < 3 * nb) return hipErrorInvalidValue;
     k_prox_rhs<<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb, gath_crit,

@@ -42,6 +42,28 @@ inline std::vector<Xfer> halo_xfers(int Nt, int64_t nxy, int W) {
     return xs;
 }
 
+// `depth` halo planes on each side (planes -depth .. -1 and nloc .. nloc + depth - 1 of every
+// rank), each from the rank that owns that global plane (a rank with fewer planes than depth
+// gets some of its halo from two ranks away); planes outside [0, Nt) are not sent.  depth 1
+// is halo_xfers' list in a different order; the fused prox + RHS reads phi two planes deep.
+inline std::vector<Xfer> halo_depth_xfers(int Nt, int64_t nxy, int W, int depth) {
+    std::vector<int> t0(W), nl(W), owner(Nt);
+    for (int g = 0; g < W; ++g) {
+        split_planes(Nt, W, g, &t0[g], &nl[g]);
+        for (int t = t0[g]; t < t0[g] + nl[g]; ++t) owner[t] = g;
+    }
+    std::vector<Xfer> xs;
+    for (int b = 0; b < W; ++b)
+        for (int k = 0; k < 2 * depth; ++k) {
+            const int h = (k < depth) ? k - depth : nl[b] + (k - depth);   // local halo plane of rank b
+            const int t = t0[b] + h;
+            if (t < 0 || t >= Nt) continue;
+            const int a = owner[t];
+            xs.push_back({a, b, (int64_t)(t - t0[a]) * nxy, (int64_t)h * nxy, nxy});
+        }
+    return xs;
+}
+
 // all-to-all between the physical slabs and the spectral row boxes (SpectralPlan):
 //   forward : rank a sends stage_a[na*Nx*y0_b, + na*nyl_b*Nx]   -> box_in_b[t0_a*nyl_b*Nx, ...]
 //   backward: rank a sends box_out_a[t0_b*nyl_a*Nx, + nb*nyl_a*Nx] -> stage_b[nb*Nx*y0_a, ...]

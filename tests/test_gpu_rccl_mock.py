@@ -124,3 +124,21 @@ def test_rccl_path_bench_grid_w8(cg_mode):
     one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=3, cg_mode=cg_mode)
     assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
     np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)
+
+
+def test_rccl_path_c4_w8():
+    """BASELINE config 4 (1024 x 1024 x 64, time-sharded over 8 GPUs) through the RCCL branches:
+    8 planes and 128 rows per rank, the default Gauss CG (one histogram all-gather per solve),
+    the fused prox + RHS with its two-plane phi / one-plane mu halos.  Bit-identical to the same
+    decomposition as virtual ranks; CG counts within one of a single shard's."""
+    from foto.synthetic import translating_gaussian
+    Nt, Nx, Ny, W = 64, 1024, 1024, 8
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+    one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
+    assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
+    np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)
+    assert all(r["redo"] == 0 for r in ranks)

@@ -19,7 +19,7 @@ import ctypes
 import numpy as np
 import pytest
 
-XFER_HALO, XFER_SLAB_TO_BOX, XFER_BOX_TO_SLAB, XFER_RELAY, XFER_DELIVER = range(5)
+XFER_HALO, XFER_SLAB_TO_BOX, XFER_BOX_TO_SLAB, XFER_RELAY, XFER_DELIVER, XFER_HALO2 = range(6)
 SEND, RECV, COPY = range(3)
 
 GRIDS = [(32, 480, 640), (32, 388, 584), (64, 1024, 1024)]   # (Nt, Ny, Nx)
@@ -51,6 +51,8 @@ def src_extent(kind, Nt, Ny, Nx, W, g):
     _, nyl = split(Ny, W, g)
     if kind == XFER_HALO:
         return -nxy, (nl + 1) * nxy
+    if kind == XFER_HALO2:
+        return 0, nl * nxy                      # own planes only (halos come from their owners)
     if kind == XFER_SLAB_TO_BOX:
         return 0, nl * nxy                      # stage: [h][tl][rows of h][x]
     if kind == XFER_BOX_TO_SLAB:
@@ -64,6 +66,8 @@ def dst_extent(kind, Nt, Ny, Nx, W, g):
     _, nyl = split(Ny, W, g)
     if kind == XFER_HALO:
         return -nxy, (nl + 1) * nxy
+    if kind == XFER_HALO2:
+        return -2 * nxy, (nl + 2) * nxy
     if kind == XFER_SLAB_TO_BOX:
         return 0, max(Nt * nyl * Nx, nl * nxy)   # box_in (the spectral tmp buffer)
     if kind == XFER_BOX_TO_SLAB:
@@ -120,7 +124,7 @@ def check_bounds_and_tiling(kind, cs, Nt, Ny, Nx, W, expect_full):
 def test_rccl_call_sequences_pair(grid, W):
     Nt, Ny, Nx = grid
     nxy = Nx * Ny
-    for kind in (XFER_HALO, XFER_SLAB_TO_BOX, XFER_BOX_TO_SLAB, XFER_DELIVER):
+    for kind in (XFER_HALO, XFER_HALO2, XFER_SLAB_TO_BOX, XFER_BOX_TO_SLAB, XFER_DELIVER):
         cs = all_calls(kind, Nt, Ny, Nx, W)
         check_pairing(cs, W)
         if kind == XFER_SLAB_TO_BOX:
@@ -137,6 +141,14 @@ def test_rccl_call_sequences_pair(grid, W):
         recv = sorted((c[1], c[2], c[3]) for c in cs[g] if c[0] == RECV)
         want = sorted(([(g - 1, -nxy, nxy)] if g > 0 else []) + ([(g + 1, nl * nxy, nxy)] if g + 1 < W else []))
         assert recv == want
+    # two-plane halo (phi of the fused prox + RHS): each halo plane from the rank owning it
+    cs = all_calls(XFER_HALO2, Nt, Ny, Nx, W)
+    owner = [g for g in range(W) for _ in range(split(Nt, W, g)[1])]
+    for g in range(W):
+        t0, nl = split(Nt, W, g)
+        got = sorted([(c[1], c[2]) for c in cs[g] if c[0] == RECV] + [(g, c[4]) for c in cs[g] if c[0] == COPY])
+        want = sorted((owner[t0 + h], h * nxy) for h in (-2, -1, nl, nl + 1) if 0 <= t0 + h < Nt)
+        assert got == want
     # relay: only ranks j and j + 1 take part, one plane of positions
     for j in range(W - 1):
         cs = all_calls(XFER_RELAY, Nt, Ny, Nx, W, j)
@@ -220,6 +232,21 @@ def test_replayed_exchanges_move_the_right_elements(shape, W):
             np.testing.assert_array_equal(f[0], G[t0 - 1].ravel())
         if g + 1 < W:
             np.testing.assert_array_equal(f[nl + 1], G[t0 + nl].ravel())
+
+    # two-plane halos (planes -2, -1, nloc, nloc + 1), from two ranks away when a slab is one plane
+    fields2 = {}
+    for g, (t0, nl) in enumerate(slabs):
+        f = np.full((nl + 4) * nxy, np.nan)
+        f[2 * nxy:(nl + 2) * nxy] = G[t0:t0 + nl].ravel()
+        fields2[g] = (f, 2 * nxy)
+    replay(XFER_HALO2, Nt, Ny, Nx, W, fields2, fields2)
+    for g, (t0, nl) in enumerate(slabs):
+        f = fields2[g][0].reshape(nl + 4, nxy)
+        for h in (-2, -1, nl, nl + 1):
+            if 0 <= t0 + h < Nt:
+                np.testing.assert_array_equal(f[h + 2], G[t0 + h].ravel())
+            else:
+                assert np.all(np.isnan(f[h + 2]))
 
     # trajectory relay j -> j + 1 and the flow delivery W - 1 -> 0
     pos = {g: (np.full(nxy, float(g)), 0) for g in range(W)}
