@@ -266,18 +266,23 @@ def test_sharded_solver_matches_oracle(W):
 
 
 def _rdv_worker(rank, W, port, q):
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=W)
-    obj = [os.urandom(128) if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)   # bench.py: RCCL unique id from rank 0
-    t = torch.tensor([0.5 + rank], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)   # bench.py: max-over-ranks timing
-    dist.barrier()
-    q.put((rank, obj[0], float(t.item())))
-    dist.destroy_process_group()
+    """bench.py's rendezvous as the driver's launch sees it: ranks that are children of one
+    launcher process, MASTER_PORT in the environment, no torch.distributed."""
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, REPO)
+    import bench
+    rdv = bench.FileRendezvous(rank, W, timeout=60)
+    nid = rdv.broadcast("nccl_id", os.urandom(128) if rank == 0 else None)   # RCCL unique id from rank 0
+    rdv.barrier()
+    m = rdv.max(0.5 + rank)                                                  # max-over-ranks timing
+    rdv.barrier()
+    m2 = rdv.max(10.0 - rank)
+    rdv.close()
+    q.put((rank, nid, m, m2))
 
 
-def test_bench_rendezvous_gloo():
-    W = 2
+@pytest.mark.parametrize("W", [2, 3])
+def test_bench_rendezvous_files(W):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -291,6 +296,10 @@ def test_bench_rendezvous_gloo():
     ids = {r[1] for r in res}
     assert len(ids) == 1 and len(next(iter(ids))) == 128
     assert all(r[2] == 0.5 + (W - 1) for r in res)
+    assert all(r[3] == 10.0 for r in res)
+    import bench
+    key = f"foto_bench_{port}_{os.getpid()}"
+    assert not os.path.exists(os.path.join(__import__("tempfile").gettempdir(), key))   # rank 0 cleaned up
 
 
 # ---------------------------------------------------------------- spectral s-step CG over slabs

@@ -46,6 +46,9 @@ def _run(s, its):
     (16, 96, 80, 2, 1, 8),        # s-step, fused prox + RHS
     (16, 96, 80, 2, 2, 6),        # s-step, two in-process shards (the RCCL transfer lists)
     (32, 640, 480, 2, 1, 4),      # bench grid: ring pass, wave-pair t-axis columns
+    (16, 96, 80, 3, 1, 8),        # Gauss CG (the default), two iterations in flight
+    (16, 96, 80, 3, 2, 6),        # Gauss CG, two in-process shards (one histogram all-gather)
+    (32, 640, 480, 3, 1, 4),      # bench grid, Gauss CG: the column-kernel t axis
 ])
 def test_reset_bit_identical(Nt, Nx, Ny, mode, vr, its):
     a0, a1 = _pair(Nx, Ny, 1)
@@ -67,6 +70,29 @@ def test_reset_bit_identical(Nt, Nx, Ny, mode, vr, its):
         # solve has launched when the host sees it finish depends on host timing, not on state
         counts = lambda st: {k: v["n"] for k, v in st["kernels"].items() if k != "spec_cg"}  # noqa: E731
         assert counts(got["st"]) == counts(fresh["st"])
+
+
+@pytest.mark.parametrize("vr", [1, 2])
+def test_reset_after_gauss_fallback(monkeypatch, vr):
+    """A context whose Gauss solves fell back to the s-step CG (FOTO_GQ_KLIM forces status 2:
+    the done chain is broken, then cleared by the redo) and is then reset solves the next pair
+    with the bits of a fresh context."""
+    Nt, Nx, Ny, its = 16, 96, 80, 6
+    a0, a1 = _pair(Nx, Ny, 1)
+    b0, b1 = _pair(Nx, Ny, 2, shift=3)
+    monkeypatch.delenv("FOTO_GQ_KLIM", raising=False)
+    with BBSolver(b0, b1, Nt, Nx, Ny, cg_mode=3, virtual_ranks=vr) as s:
+        fresh = _run(s, its)
+    with BBSolver(a0, a1, Nt, Nx, Ny, cg_mode=3, virtual_ranks=vr) as s:
+        monkeypatch.setenv("FOTO_GQ_KLIM", "5")
+        forced = _run(s, its)
+        assert forced["st"]["cg_redo"] == its
+        monkeypatch.delenv("FOTO_GQ_KLIM")
+        s.reset(b0, b1)
+        reused = _run(s, its)
+    assert reused["st"]["cg_redo"] == 0
+    for k in ("u", "v", "m", "phi", "crit", "cg"):
+        assert np.array_equal(reused[k], fresh[k]), k
 
 
 def test_solve_reuses_context(monkeypatch):
