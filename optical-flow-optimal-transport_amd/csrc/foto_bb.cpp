@@ -171,7 +171,8 @@ struct foto_bb_ctx {
     bool pipe = false;
     struct Enq {            // an outer iteration on the stream (outer_tail -> outer_complete)
         int par = 0;        // its event / readback slot
-        SpectralPlan* dsp = nullptr;   // deferred solve to finish
+        SpectralPlan* dsp = nullptr;   // deferred solve to finish (single shard)
+        bool sdefer = false;           // sharded Gauss solve enqueued without a host wait
         int its = 0, info = 0;         // a synchronous solve's result
         size_t kmark = 0;              // KTimer mark before its launches
         // host state before it (restored by a rollback)
@@ -403,39 +404,41 @@ static int alltoall_spec(foto_bb_ctx* c, bool forward) {
     return exchange(c, alltoall_xfers(c->Nt, c->Ny, c->Nx, c->W, forward), sbuf, rbuf);
 }
 
-// Spectral s-step CG over time-slab shards: x/y DCTs on the own planes, all-to-all to
-// row boxes, t-DCT, pointwise CG passes with one NACC-double all-gather each (moments summed
-// in rank order on every rank, so all ranks plan identically), then back.
-static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
-    const int maxiter = c->o.cg_maxiter;
-    const double rtol = c->o.cg_rtol;
-    const int M = SpectralPlan::moments();
+// Spectral CG over time-slab shards, in phases: x/y DCTs on the own planes, all-to-all to row
+// boxes and the t-DCT (sharded_fwd); the Gauss-compressed CG -- one all-gather of the boxes'
+// histograms, summed in rank order on every rank, and the small serial solve on every rank
+// (sharded_gauss) -- or the s-step CG from b^ with one NACC-double all-gather per pass (moments
+// summed in rank order, so all ranks plan identically; sharded_sstep); then x^, the inverse
+// t-DCT, the all-to-all back and the inverse x/y DCTs (sharded_inv).
+static int sharded_fwd(foto_bb_ctx* c) {
     KTimer* kt = &c->kt;
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_local(sp->rv, kt, c->s));
     FOTO_TRY(alltoall_spec(c, true));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_t(kt, c->s));
-    if (c->sh[0]->spec->gauss()) {
-        // Gauss-compressed CG: one all-gather of the boxes' histograms (summed in rank order on
-        // every rank), the small serial solve on every rank, the inverse from the table
-        for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_measure(kt, c->s));
-        FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gauss_hist(); }, SpectralPlan::gauss_hist_size()));
-        for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_solve(rtol, maxiter, kt, c->s));
-        int ok = 1;
-        for (auto& sp : c->sh) {
-            int k_ok = 0;
-            FOTO_TRY(sp->spec->gauss_wait(maxiter, &k_ok, iters, info, c->s));
-            ok = ok && k_ok;   // identical on every shard and rank (same gathered histograms)
-        }
-        if (ok) {
-            for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
-            for (auto& sp : c->sh) sp->spec->gauss_end();
-            FOTO_TRY(alltoall_spec(c, false));
-            for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
-            c->last_cg = *iters;
-            return 0;
-        }
-        c->st.cg_redo += 1;   // the s-step CG from b^ (cg_begin takes its INIT moments)
-    }
+    return 0;
+}
+
+static int sharded_gauss(foto_bb_ctx* c) {
+    KTimer* kt = &c->kt;
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_measure(kt, c->s));
+    FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gauss_hist(); }, SpectralPlan::gauss_hist_size()));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->gauss_solve(c->o.cg_rtol, c->o.cg_maxiter, kt, c->s));
+    return 0;
+}
+
+static int sharded_inv(foto_bb_ctx* c) {
+    KTimer* kt = &c->kt;
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
+    FOTO_TRY(alltoall_spec(c, false));
+    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
+    return 0;
+}
+
+static int sharded_sstep(foto_bb_ctx* c, int* iters, int* info) {
+    const int maxiter = c->o.cg_maxiter;
+    const double rtol = c->o.cg_rtol;
+    const int M = SpectralPlan::moments();
+    KTimer* kt = &c->kt;
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_begin(rtol, maxiter, kt, c->s));
     FOTO_TRY(allgather(c, [](Shard& s) { return s.spec->gath(); }, M));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->cg_plan(1, rtol, maxiter, c->s));
@@ -455,14 +458,36 @@ static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
             return FOTO_ERR_STATE;
         }
     }
-    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
-    FOTO_TRY(alltoall_spec(c, false));
-    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
     *iters = its;
     *info = (done == 1) ? 0 : maxiter;
-    c->last_cg = its;
     c->last_passes = planned;
     kt->discard_last(FOTO_K_SPEC, std::max(0, passes - planned) * (int)c->sh.size());   // no-op passes
+    return 0;
+}
+
+// the whole sharded solve, waiting for it on the host (FOTO_CG_DEFER=0, or the s-step CG)
+static int cg_solve_spectral_sharded(foto_bb_ctx* c, int* iters, int* info) {
+    const int maxiter = c->o.cg_maxiter;
+    FOTO_TRY(sharded_fwd(c));
+    if (c->sh[0]->spec->gauss()) {
+        FOTO_TRY(sharded_gauss(c));
+        int ok = 1;
+        for (auto& sp : c->sh) {
+            int k_ok = 0;
+            FOTO_TRY(sp->spec->gauss_wait(maxiter, &k_ok, iters, info, c->s));
+            ok = ok && k_ok;   // identical on every shard and rank (same gathered histograms)
+        }
+        if (ok) {
+            FOTO_TRY(sharded_inv(c));
+            for (auto& sp : c->sh) sp->spec->gauss_end();
+            c->last_cg = *iters;
+            return 0;
+        }
+        c->st.cg_redo += 1;   // the s-step CG from b^ (cg_begin takes its INIT moments)
+    }
+    FOTO_TRY(sharded_sstep(c, iters, info));
+    FOTO_TRY(sharded_inv(c));
+    c->last_cg = *iters;
     return 0;
 }
 
@@ -536,8 +561,9 @@ static int outer_head(foto_bb_ctx* c) {
 }
 
 // the fused k_prox_rhs of every local shard on the pair recorded in its fz_src -> fz_dst;
-// sharded: the two-plane phi halo and the one-plane halo of the mu it reads go first
-static int prox_rhs(foto_bb_ctx* c, const int* guard) {
+// sharded: the two-plane phi halo and the one-plane halo of the mu it reads go first.
+// guarded: each shard's launch returns at once unless its CG's done flag is set.
+static int prox_rhs(foto_bb_ctx* c, bool guarded) {
     const int W = c->W;
     if (W > 1) {
         FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
@@ -550,7 +576,8 @@ static int prox_rhs(foto_bb_ctx* c, const int* guard) {
         hipEvent_t e = c->kt.start(c->s);
         FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.fz_dst[0], s.fz_dst[1],
                                        s.fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(W) + 2 * s.rank,
-                                       c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s, guard));
+                                       c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s,
+                                       guarded ? s.spec->done_flag() : nullptr));
         c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
     }
     // the stencil CG's F.F (its stopping rule) from every rank
@@ -590,12 +617,22 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
         set_error("outer iteration: the pipelined loop needs a deferrable Gauss solve");
         return FOTO_ERR_STATE;
     }
+    // Sharded Gauss CG: likewise enqueued whole -- x^ from the table, the all-to-all back, the
+    // inverse DCTs and prox (guarded by each shard's done flag) -- and checked at the crit sync;
+    // a failed solve (every rank sees the same status: the same gathered histograms) is redone
+    // there with the s-step CG from b^ by every rank, so the collective sequence stays identical
+    const bool sdefer = defer_on && W > 1 && s0.spec && s0.spec->gauss();
     if (c->pipe) std::swap(s0.phi, s0.phi_alt);   // this iteration's phi; the last one's stays intact
     if (dsp) {
         FOTO_TRY(dsp->solve_deferred(s0.rv, s0.phi, c->o.cg_rtol, c->o.cg_maxiter, &c->kt, c->s));
+    } else if (sdefer) {
+        FOTO_TRY(sharded_fwd(c));
+        FOTO_TRY(sharded_gauss(c));
+        FOTO_TRY(sharded_inv(c));
     } else {
         FOTO_TRY(cg_solve(c, &e.its, &e.info));
     }
+    const bool guarded = dsp != nullptr || sdefer;
     FOTO_HIP_CHECK(hipEventRecord(ph[2], c->s));
     c->have_phi = 1;
 
@@ -604,7 +641,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
         // (pipelined: mu -> nu -> xi -> mu rotate, so the mu before this iteration survives it)
         for (auto& sp : c->sh)
             for (int f = 0; f < 3; ++f) { sp->fz_src[f] = sp->mu[f]; sp->fz_dst[f] = sp->nu[f]; }
-        FOTO_TRY(prox_rhs(c, dsp ? dsp->done_flag() : nullptr));
+        FOTO_TRY(prox_rhs(c, guarded));
         for (auto& sp : c->sh)
             for (int f = 0; f < 3; ++f) {
                 if (c->pipe) {
@@ -624,7 +661,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
             hipEvent_t t = c->kt.start(c->s);
             FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r, s.rb,
-                                       s.gath_crit(W), s.rank, c->s, dsp ? dsp->done_flag() : nullptr));
+                                       s.gath_crit(W), s.rank, c->s, guarded ? s.spec->done_flag() : nullptr));
             c->kt.stop(t, c->s, FOTO_K_PROX, 80.0 * nv);
         }
     }
@@ -632,6 +669,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s0.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
     FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
     e.dsp = dsp;
+    e.sdefer = sdefer;
     c->inflight.push_back(e);
     return 0;
 }
@@ -689,7 +727,7 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
             c->kt.discard_last(FOTO_K_PROX, 1);
             if (c->fuse) {
-                FOTO_TRY(prox_rhs(c, nullptr));
+                FOTO_TRY(prox_rhs(c, false));
                 c->f_ready = true;   // (a rollback before the redo had cleared it)
             } else {
                 hipEvent_t t = c->kt.start(c->s);
@@ -702,6 +740,38 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
             c->st.cg_redo += 1;
         }
+    }
+    if (e.sdefer) {
+        int ok = 1;
+        for (auto& sp : c->sh) {
+            int k_ok = 0;
+            FOTO_TRY(sp->spec->gauss_result(c->o.cg_maxiter, &k_ok, cg_iters, cg_info, c->s));
+            ok = ok && k_ok;   // identical on every shard and rank
+        }
+        if (!ok) {
+            // every rank: the s-step CG from b^ (still intact: x^ went to the box scratch), the
+            // inverse again, then the prox that the done flags held back, and a new crit readback
+            c->kt.discard_last(FOTO_K_PROX, (int)c->sh.size());
+            FOTO_TRY(sharded_sstep(c, cg_iters, cg_info));
+            FOTO_TRY(sharded_inv(c));
+            if (c->fuse) {
+                FOTO_TRY(prox_rhs(c, false));
+            } else {
+                FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+                for (auto& sp : c->sh) {
+                    Shard& s = *sp;
+                    FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r,
+                                               s.rb, s.gath_crit(W), s.rank, c->s));
+                }
+            }
+            FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
+            FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], c->sh[0]->gath, sizeof(double) * 4 * W,
+                                          hipMemcpyDeviceToHost, c->s));
+            FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
+            FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
+            c->st.cg_redo += 1;
+        }
+        c->last_cg = *cg_iters;
     }
     float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
     FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, ph[0], ph[1]));

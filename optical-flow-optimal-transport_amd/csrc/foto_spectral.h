@@ -54,6 +54,9 @@ struct SpectralPlan {
     int gauss_measure(KTimer* kt, hipStream_t s);
     int gauss_solve(double rtol, int maxiter, KTimer* kt, hipStream_t s);
     int gauss_wait(int maxiter, int* ok, int* iters, int* info, hipStream_t s);
+    // gauss_wait without the sync (the caller has waited past the solve's header copy); ends the
+    // Gauss solve either way (!ok: the caller redoes it with the s-step CG)
+    int gauss_result(int maxiter, int* ok, int* iters, int* info, hipStream_t s);
     void gauss_end();
 
     // back to the state init() leaves (no solve in flight, no pass-count prediction, the

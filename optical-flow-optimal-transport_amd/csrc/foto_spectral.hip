@@ -618,6 +618,9 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 #ifndef FOTO_FFT_LPB_MAX
 #define FOTO_FFT_LPB_MAX 64
 #endif
+#ifndef FOTO_FFT_LPB_CONTIG_MAX
+#define FOTO_FFT_LPB_CONTIG_MAX 64   // contiguous (x-axis) lines per block cap (A/B builds)
+#endif
 #ifndef FOTO_FFT_SYM
 #define FOTO_FFT_SYM 1         // odd prime-length codelets by symmetric pairs (0: direct codelets)
 #endif
@@ -638,7 +641,8 @@ struct FftGeom {
         const int c[8] = {64, 32, 16, 12, 8, 4, 2, 1};
         const int budget = CONTIG ? 65536 : FOTO_FFT_STRIDED_LDS;
         for (int i = 0; i < 8; ++i)
-            if (c[i] <= FOTO_FFT_LPB_MAX && !(FOTO_FFT_LPB_POW2 && c[i] == 12) &&
+            if (c[i] <= FOTO_FFT_LPB_MAX && (!CONTIG || M2 > 32 || c[i] <= FOTO_FFT_LPB_CONTIG_MAX) &&
+                !(FOTO_FFT_LPB_POW2 && c[i] == 12) &&
                 c[i] * LS * 8 + (FOTO_FFT_TW_LDS ? 16 * M : 0) <= budget)
                 return c[i];
         return 1;
@@ -3743,6 +3747,15 @@ int SpectralPlan::gauss_wait(int maxiter, int* ok, int* iters, int* info, hipStr
         P->gauss_active = false;
         FOTO_TRY(gq_unbreak(P, s));   // the s-step CG redoes this solve (foto_bb.cpp)
     }
+    return 0;
+}
+
+int SpectralPlan::gauss_result(int maxiter, int* ok, int* iters, int* info, hipStream_t s) {
+    SpecImpl* P = (SpecImpl*)impl;
+    *ok = P->hgq2[P->hlast]->status == 0;
+    gq_result(P, P->hlast, maxiter, iters, info);
+    P->gauss_active = false;
+    if (!*ok) FOTO_TRY(gq_unbreak(P, s));
     return 0;
 }
 

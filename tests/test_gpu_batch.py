@@ -77,13 +77,14 @@ def test_reset_after_gauss_fallback(monkeypatch, vr):
     """A context whose Gauss solves fell back to the s-step CG (FOTO_GQ_KLIM forces status 2:
     the done chain is broken, then cleared by the redo) and is then reset solves the next pair
     with the bits of a fresh context."""
-    Nt, Nx, Ny, its = 16, 96, 80, 6
+    Nt, Nx, Ny, its, eps = 16, 96, 80, 6, 1e-2   # (eps 1e-3: this noisy pair needs K > 512 anyway)
     a0, a1 = _pair(Nx, Ny, 1)
     b0, b1 = _pair(Nx, Ny, 2, shift=3)
     monkeypatch.delenv("FOTO_GQ_KLIM", raising=False)
-    with BBSolver(b0, b1, Nt, Nx, Ny, cg_mode=3, virtual_ranks=vr) as s:
+    with BBSolver(b0, b1, Nt, Nx, Ny, reg_epsilon=eps, cg_mode=3, virtual_ranks=vr) as s:
         fresh = _run(s, its)
-    with BBSolver(a0, a1, Nt, Nx, Ny, cg_mode=3, virtual_ranks=vr) as s:
+    assert fresh["st"]["cg_redo"] == 0
+    with BBSolver(a0, a1, Nt, Nx, Ny, reg_epsilon=eps, cg_mode=3, virtual_ranks=vr) as s:
         monkeypatch.setenv("FOTO_GQ_KLIM", "5")
         forced = _run(s, its)
         assert forced["st"]["cg_redo"] == its

@@ -20,7 +20,7 @@ from foto.bb import BBSolver  # noqa: E402
 
 
 def _run(d, monkeypatch, env, calls, **kw):
-    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM"):
+    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM", "FOTO_CG_DEFER"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -101,3 +101,26 @@ def test_pipe_exact_iteration_count(gold, monkeypatch):
     _same(a, b)
     _same(a, c)
     assert len(a["crit"]) == 7 and a["stats"]["outer_iters"] == 7
+
+
+@pytest.mark.parametrize("klim", ["1", "200", None])
+@pytest.mark.parametrize("vr", [2, 3])
+def test_sharded_gauss_deferred(gold, monkeypatch, vr, klim):
+    """Sharded Gauss CG enqueued whole (x^, all-to-all back, inverse DCTs and the prox guarded by
+    each shard's done flag) and checked at the crit sync; a failed solve (FOTO_GQ_KLIM) is redone
+    there with the s-step CG from b^ by every shard.  Bit-identical to the sharded solve waited
+    for on the host (FOTO_CG_DEFER=0), which redoes the same solves before the inverse."""
+    d = gold("bb_c1.npz")
+    max_it = int(d["params"][3])
+    env = {} if klim is None else {"FOTO_GQ_KLIM": klim}
+    a = _run(d, monkeypatch, env, [(max_it, None, True)], virtual_ranks=vr)
+    b = _run(d, monkeypatch, {**env, "FOTO_CG_DEFER": "0"}, [(max_it, None, True)], virtual_ranks=vr)
+    monkeypatch.delenv("FOTO_CG_DEFER", raising=False)
+    _same(a, b)
+    n = len(a["crit"])
+    assert n == len(d["crit"])
+    assert a["stats"]["cg_redo"] == b["stats"]["cg_redo"]
+    if klim == "1":
+        assert a["stats"]["cg_redo"] == n
+    assert np.max(np.abs(a["its"] - d["cg_its"])) <= 1
+    np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)

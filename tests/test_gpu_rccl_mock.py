@@ -98,6 +98,21 @@ def test_rccl_path_bit_identical_to_virtual_ranks(W, cg_mode):
     compare(ranks, virt, Nt, Nx, Ny, W)
 
 
+def test_rccl_path_gauss_redo(monkeypatch):
+    """A failed Gauss solve on every rank (FOTO_GQ_KLIM=1: status 2 everywhere, from the same
+    gathered histograms) is redone by every rank with the s-step CG at the crit sync: the
+    collective sequences stay paired and the results equal the virtual ranks' bit for bit."""
+    from foto.synthetic import translating_gaussian
+    monkeypatch.setenv("FOTO_GQ_KLIM", "1")
+    Nt, Nx, Ny, W = 16, 64, 48, 3
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+    assert all(r["redo"] == 4 for r in ranks)
+
+
 def test_rccl_path_stencil_cg():
     """cg_mode 0: a halo exchange of p and two scalar all-gathers per CG iteration."""
     from foto.synthetic import translating_gaussian
