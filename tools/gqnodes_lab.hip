@@ -24,16 +24,23 @@ using namespace foto;
 
 // the root finder of k_gq_nodes with counters: out[id] = bisections | newton << 10 | fallback << 20
 __global__ __launch_bounds__(64) void k_nodes_count(const double* __restrict__ hist, const GqExact* __restrict__ X,
-                                                    int* __restrict__ out) {
+                                                    int* __restrict__ out, long long* __restrict__ clk) {
     const int id = blockIdx.x * 64 + threadIdx.x;
     if (id >= GQ_NODES) return;
+    const long long c0 = __builtin_amdgcn_s_memtime();
     const int bin = id / GQ_M, k = id - bin * GQ_M;
     double mu[GQ_NM];
 #pragma unroll
     for (int j = 0; j < GQ_NM; ++j) mu[j] = hist[j * GQ_NB + bin];
     if (X->n[bin] <= GQ_XS) { out[id] = -1; return; }
     double al[GQ_M], be[GQ_M];
+    double msum = 0.0;
+#pragma unroll
+    for (int j = 0; j < GQ_NM; ++j) msum += mu[j];
+    const long long c1 = __builtin_amdgcn_s_memtime() + (msum == 12345.678 ? 1 : 0);
     const int n = gq_mcheb(mu, al, be);
+    const long long c2 = __builtin_amdgcn_s_memtime() + (al[GQ_M - 1] == 12345.678 ? 1 : 0);
+    long long c3 = c2, c4 = c2;
     int nb = 0, nn = 0, fb = 0;
     if (k < n) {
         double sb[GQ_M];
@@ -61,6 +68,7 @@ __global__ __launch_bounds__(64) void k_nodes_count(const double* __restrict__ h
             }
         };
         bisect(24, 96);
+        c3 = __builtin_amdgcn_s_memtime() + (lo == 12345.678 ? 1 : 0);
         double u = 0.5 * (lo + hi);
         bool ok = true;
         for (int it = 0; it < 6; ++it) {
@@ -81,8 +89,10 @@ __global__ __launch_bounds__(64) void k_nodes_count(const double* __restrict__ h
             u = un;
         }
         if (!ok) { fb = 1; bisect(200, 200); }
+        c4 = __builtin_amdgcn_s_memtime() + (u == 12345.678 ? 1 : 0);
     }
     out[id] = nb | (nn << 10) | (fb << 20);
+    if (id == 0) { clk[0] = c1 - c0; clk[1] = c2 - c1; clk[2] = c3 - c2; clk[3] = c4 - c3; }
 }
 
 int main(int argc, char** argv) {
@@ -142,7 +152,12 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, e));
     printf("k_gq_nodes: %.2f us per launch (decay %.1f)\n", 1e3 * ms / reps, decay);
-    k_nodes_count<<<GQ_NODES / 64, 64>>>(dh, X, cnt);
+    long long* clk;
+    CK(hipMalloc(&clk, 4 * sizeof(long long)));
+    k_nodes_count<<<GQ_NODES / 64, 64>>>(dh, X, cnt, clk);
+    long long hc[4];
+    CK(hipMemcpy(hc, clk, sizeof(hc), hipMemcpyDeviceToHost));
+    printf("thread 0 cycles (s_memtime): loads %lld, mcheb %lld, bisect %lld, newton %lld\n", hc[0], hc[1], hc[2], hc[3]);
     std::vector<int> c(GQ_NODES);
     CK(hipMemcpy(c.data(), cnt, sizeof(int) * GQ_NODES, hipMemcpyDeviceToHost));
     int hb[8] = {0}, fbs = 0, maxb = 0, maxn = 0, wave_max_sum = 0;
