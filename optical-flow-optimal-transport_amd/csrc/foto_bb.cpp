@@ -99,6 +99,10 @@ struct Shard {
     // the last fused prox + RHS launch's mu in / out (fz_src is the mu stepB of phi used)
     double* fz_src[3] = {nullptr, nullptr, nullptr};
     double* fz_dst[3] = {nullptr, nullptr, nullptr};
+    // sharded fused prox with deferred edges: w_t next to the slab edges (halo-padded) and the
+    // edge planes' (w_x, w_y, mu'_t, q_t), slot 0 = plane 0, slot 1 = plane nloc - 1
+    double* wt = nullptr;
+    double* edge = nullptr;
     double* rv = nullptr;    // CG residual (starts as F)
     double* p[2] = {nullptr, nullptr};
     double* rho0 = nullptr;
@@ -313,6 +317,13 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         if (c->pipe) {
             for (int f = 0; f < 3; ++f) FOTO_TRY(s.alloc_field(&s.xi[f], c->s));
             FOTO_TRY(s.alloc_field(&s.phi_alt, c->s, 2));
+        }
+        if (c->fuse && W > 1) {
+            FOTO_TRY(s.alloc_field(&s.wt, c->s));
+            void* eb = nullptr;
+            FOTO_TRY(s.alloc(sizeof(double) * 8 * nxy, &eb));
+            FOTO_HIP_CHECK(hipMemsetAsync(eb, 0, sizeof(double) * 8 * nxy, c->s));
+            s.edge = (double*)eb;
         }
         FOTO_TRY(s.alloc_field(&s.phi, c->s, 2));
         FOTO_TRY(s.alloc_field(&s.rv, c->s));
@@ -565,20 +576,43 @@ static int outer_head(foto_bb_ctx* c) {
 // guarded: each shard's launch returns at once unless its CG's done flag is set.
 static int prox_rhs(foto_bb_ctx* c, bool guarded) {
     const int W = c->W;
+    // sharded: defer the slab-edge F (default: two planes per neighbour on the wire, phi and w_t)
+    // or recompute the neighbours' boundary stepB (FOTO_PR_EDGE=0: five planes, 2 phi + 3 mu)
+    const char* pe = getenv("FOTO_PR_EDGE");
+    const bool defer = W > 1 && !(pe && atoi(pe) == 0);
     if (W > 1) {
-        FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
-                          [](Shard& s) { return s.phi; }));
-        for (int f = 0; f < 3; ++f) FOTO_TRY(halo(c, [f](Shard& s) { return s.fz_src[f]; }));
+        if (defer) {
+            FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+        } else {
+            FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
+                              [](Shard& s) { return s.phi; }));
+            for (int f = 0; f < 3; ++f) FOTO_TRY(halo(c, [f](Shard& s) { return s.fz_src[f]; }));
+        }
     }
     for (auto& sp : c->sh) {
         Shard& s = *sp;
         const double nv = (double)s.g.nloc * (double)s.g.nxy;
+        const int dlo = defer && s.g.t0 > 0, dhi = defer && s.g.t0 + s.g.nloc < c->Nt;
         hipEvent_t e = c->kt.start(c->s);
         FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.fz_dst[0], s.fz_dst[1],
                                        s.fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(W) + 2 * s.rank,
                                        c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s,
-                                       guarded ? s.spec->done_flag() : nullptr));
+                                       guarded ? s.spec->done_flag() : nullptr, dlo, dhi, s.wt, s.edge));
         c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
+    }
+    if (defer) {
+        FOTO_TRY(halo(c, [](Shard& s) { return s.wt; }));
+        for (auto& sp : c->sh) {
+            Shard& s = *sp;
+            const int dlo = s.g.t0 > 0, dhi = s.g.t0 + s.g.nloc < c->Nt;
+            double* rr = c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr;
+            const int* gd = guarded ? s.spec->done_flag() : nullptr;
+            if (dlo)
+                FOTO_HIP_CHECK(launch_rhs_edge(s.g, 0, s.wt, s.edge, s.rho0, s.rhoT, c->r, s.rv, s.rb, rr, c->s, gd));
+            if (dhi && !(dlo && s.g.nloc == 1))
+                FOTO_HIP_CHECK(launch_rhs_edge(s.g, s.g.nloc - 1, s.wt, s.edge + 4 * s.g.nxy, s.rho0, s.rhoT, c->r, s.rv,
+                                               s.rb, rr, c->s, gd));
+        }
     }
     // the stencil CG's F.F (its stopping rule) from every rank
     if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
@@ -1029,6 +1063,8 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
                             s.xi[0], s.xi[1], s.xi[2], s.rv, s.p[0], s.p[1]};
         for (double* f : fields)   // as ctx_init leaves them: zero, halo planes included
             if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - nxy, 0, bytes, c->s));
+        if (s.wt) FOTO_HIP_CHECK(hipMemsetAsync(s.wt - nxy, 0, bytes, c->s));
+        if (s.edge) FOTO_HIP_CHECK(hipMemsetAsync(s.edge, 0, sizeof(double) * 8 * nxy, c->s));
         for (double* f : {s.phi, s.phi_alt})   // (two halo planes per side)
             if (f) FOTO_HIP_CHECK(hipMemsetAsync(f - 2 * nxy, 0, bytes + 2 * nxy * sizeof(double), c->s));
         FOTO_HIP_CHECK(hipMemsetAsync(s.gath, 0, sizeof(double) * 4 * c->W, c->s));

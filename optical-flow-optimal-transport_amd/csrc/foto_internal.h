@@ -216,12 +216,20 @@ hipError_t launch_prox(const Geo& g, const double* phi, double* mut, double* mux
                        const int* guard = nullptr);
 // k_prox fused with the next iteration's RHS (mu -> nu, F, this rank's crit num/den ->
 // gath_crit[0..1], F.F -> gath_rr[0] when non-null); needs rb.cap >= 3 * prox_rhs_blocks(g).
-// Sharded (g.t0 > 0 or g.t0 + g.nloc < g.Nt): phi needs two valid halo planes on each side
-// and mu one (the neighbours' boundary planes), exchanged before the launch.
+// Sharded (g.t0 > 0 or g.t0 + g.nloc < g.Nt), either: defer_lo / defer_hi = 0 -- stepB is
+// recomputed on the neighbours' boundary planes: phi needs two valid halo planes on each side
+// and mu one; or defer_lo / defer_hi = 1 on the sides that have a neighbour -- phi needs one
+// halo plane, F of that edge plane is left to launch_rhs_edge after w_t's halo exchange
+// (wt_out: a halo-padded field, planes 0, 1, nloc - 2, nloc - 1 written; edge: 2 x 4 planes).
 int prox_rhs_blocks(const Geo& g);
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s,
+                           const int* guard = nullptr, int defer_lo = 0, int defer_hi = 0, double* wt_out = nullptr,
+                           double* edge = nullptr);
+// F of a deferred edge plane n (0 or nloc - 1; edge slot 0 or 1), F.F added to gath_rr[0]
+hipError_t launch_rhs_edge(const Geo& g, int n, const double* wt, const double* edge, const double* rho0,
+                           const double* rhoT, double r, double* F, RedBuf rb, double* gath_rr, hipStream_t s,
                            const int* guard = nullptr);
 // q = Proj_K(grad_st phi + mu / r) only (the stepB output the fused kernel does not store)
 hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut, const double* mux,

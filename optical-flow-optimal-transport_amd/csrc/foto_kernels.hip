@@ -711,11 +711,15 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 // a one-voxel ring (66 x 10: the x / y neighbours F needs) and on the planes l0 - 1 and l1
 // (the t neighbours), which needs phi on a two-voxel ring (68 x 12) and planes l0 - 2 .. l1 + 1.
 // mu' goes to a second buffer (neighbouring blocks still read the old mu of their ring voxels).
-// Time-sharded, a shard's first and last chunks recompute stepB on the neighbouring ranks'
-// boundary planes exactly as the chunk seams do: phi carries two halo planes and mu one on
-// each side (exchanged before the launch), so a rank's F needs nothing after its own launch.
-// Plane indices p are local (memory: p * nxy, p in [-2, nloc + 1]); t = t0 + p is global
-// (boundary conditions).  Per voxel the arithmetic is k_prox's and k_rhs's, in the same order:
+// Time-sharded there are two ways across a slab boundary.  EDGE RECOMPUTE (FOTO_PR_EDGE=0): a
+// shard's first and last chunks recompute stepB on the neighbouring ranks' boundary planes
+// exactly as the chunk seams do -- phi needs two halo planes and mu one on each side, five
+// planes per neighbour on the wire.  EDGE DEFER (default): stepB stays on the own planes, F of a
+// plane next to another rank is deferred -- the kernel stores w_t of its two outermost planes on
+// each deferred side and (w_x, w_y, mu'_t, q_t) of the edge plane itself, one w_t plane is
+// exchanged with each neighbour, and k_rhs_edge finishes F there with the same operations in the
+// same order: phi one halo plane, w_t one -- two planes per neighbour.  Plane indices p are local
+// (memory: p * nxy); t = t0 + p is global (boundary conditions).  Per voxel the arithmetic is k_prox's and k_rhs's, in the same order:
 // mu', F and the crit terms are bit-identical to the unfused kernels; only the crit / F.F sums
 // are grouped differently.
 //
@@ -742,11 +746,15 @@ constexpr int PR_FR = (PR_FN + PR_NT - 1) / PR_NT;        // phi loads per threa
 static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT,   // (32 x 16, 16 x 32, 32 x 8: slower, r03)
               "one voxel per thread, ring voxels on the first threads");
 
+// EDGE: the deferred-edge variant (sharded); the single-shard instantiation carries none of its
+// code (its extra registers spilled the kernel at the 128-VGPR cap: 171 -> 184 us)
+template <bool EDGE>
 __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_prox_rhs(
         Geo g, const double* __restrict__ phi, const double* __restrict__ mut, const double* __restrict__ mux,
         const double* __restrict__ muy, double* __restrict__ nut, double* __restrict__ nux, double* __restrict__ nuy,
         const double* __restrict__ rho0, const double* __restrict__ rhoT, double r, double inv_r,
-        double* __restrict__ F, RedBuf rb, double* gath_crit, double* gath_rr, const int* __restrict__ guard, int tch) {
+        double* __restrict__ F, RedBuf rb, double* gath_crit, double* gath_rr, const int* __restrict__ guard, int tch,
+        int defer_lo, int defer_hi, double* __restrict__ wt_out, double* __restrict__ edge) {
     if (guard && *guard == 0) return;
     __shared__ double fr[4][PR_FN];                  // phi ring (plane p in slot p & 3)
     __shared__ double wb[2][2][PR_PH * PR_PW];       // [plane & 1][x | y part] of w
@@ -783,7 +791,11 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         fin[j] = idx < PR_FN && xx >= 0 && xx < Nx && yy >= 0 && yy < Ny;
         foff[j] = fin[j] ? yy * Nx + xx : 0;
     }
-    const int pa = max(l0 - 1, -t0), pz = min(l1, Nt - 1 - t0);   // stepB planes (local; >= -1, <= nloc)
+    // stepB planes (local): one beyond the chunk on each side, within the grid and, where an edge
+    // is deferred, within the shard
+    if (!EDGE) defer_lo = defer_hi = 0;
+    const int pa = max(l0 - 1, defer_lo ? 0 : -t0), pz = min(l1, defer_hi ? g.nloc - 1 : Nt - 1 - t0);
+    const int nl = g.nloc;
     double fv[PR_FR];
     auto load_phi_to = [&](int p, double (&v)[PR_FR]) {   // planes beyond pz + 1 are never read
         const bool ok = t0 + p >= 0 && p <= pz + 1 && t0 + p < Nt;
@@ -885,7 +897,27 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         if (p <= pz) plane(p, cm, chm);
         else wtn = 0.0;   // t0 + p = Nt: F(Nt - 1) reads no w_t(Nt)
         const int n = p - 1, tn = t0 + n;
-        if (own && n >= l0) {
+        const bool deferred = (defer_lo && n == 0) || (defer_hi && n == nl - 1);   // k_rhs_edge's
+        if (EDGE && own && n >= l0) {
+            // what k_rhs_edge needs next to a deferred edge, from the values F(n) would use: w_t
+            // of the two outermost planes, and (w_x, w_y, mu'_t, q_t) of the edge plane itself
+            if ((defer_lo && n <= 1) || (defer_hi && n >= nl - 2)) wt_out[n * nxy + ooff] = wtc;
+            if (deferred) {   // slot 0: plane 0, slot 1: plane nloc - 1 (nloc = 1: both)
+                const int ci = opy * PR_PW + opx;
+                double* E = edge + ooff + ((defer_lo && n == 0) ? 0 : 4 * nxy);
+                E[0] = wb[n & 1][0][ci];
+                E[nxy] = wb[n & 1][1][ci];
+                E[2 * nxy] = bcm;
+                E[3 * nxy] = bcq;
+                if (defer_lo && defer_hi && nl == 1) {
+                    E[4 * nxy] = E[0];
+                    E[5 * nxy] = E[nxy];
+                    E[6 * nxy] = bcm;
+                    E[7 * nxy] = bcq;
+                }
+            }
+        }
+        if (own && n >= l0 && !deferred) {
             // F(n) (k_rhs's order: t, x, y terms, then the boundary-plane corrections)
             const double* WX = wb[n & 1][0];
             const double* WY = wb[n & 1][1];
@@ -929,11 +961,57 @@ int prox_rhs_blocks(const Geo& g) {
 
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
-                           double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard) {
+                           double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard,
+                           int defer_lo, int defer_hi, double* wt_out, double* edge) {
     const int nb = prox_rhs_blocks(g);
     if (rb.cap < 3 * nb) return hipErrorInvalidValue;
-    k_prox_rhs<<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb, gath_crit,
-                                    gath_rr, guard, prox_rhs_tch(g));
+    if ((defer_lo || defer_hi) && (!wt_out || !edge)) return hipErrorInvalidValue;
+    if (defer_lo || defer_hi)
+        k_prox_rhs<true><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
+                                              gath_crit, gath_rr, guard, prox_rhs_tch(g), defer_lo, defer_hi, wt_out, edge);
+    else
+        k_prox_rhs<false><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
+                                               gath_crit, gath_rr, guard, prox_rhs_tch(g), 0, 0, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+// F on a deferred edge plane of a shard (local plane n = 0 or nloc - 1) from what k_prox_rhs
+// stored there and the neighbour's w_t plane (exchanged into wt's halo): k_prox_rhs's F code
+// -- t, x, y terms, then the boundary corrections, in the same order -- so F is bit-identical
+// to the single-shard kernel's.  F.F of the plane is added to gath_rr[0] (stencil CG).
+__global__ __launch_bounds__(NT) void k_rhs_edge(Geo g, int n, const double* __restrict__ wt,
+                                                 const double* __restrict__ E, const double* __restrict__ rho0,
+                                                 const double* __restrict__ rhoT, double r, double* __restrict__ F,
+                                                 RedBuf rb, double* gath_rr, const int* __restrict__ guard) {
+    if (guard && *guard == 0) return;
+    const int64_t nxy = g.nxy;
+    const int64_t off = (int64_t)blockIdx.x * NT + threadIdx.x;
+    double ff = 0.0;
+    if (off < nxy) {
+        const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), tn = g.t0 + n;
+        const double* WX = E;
+        const double* WY = E + nxy;
+        const int64_t i = (int64_t)n * nxy + off;
+        double s = 0.0;
+        acc_d1w(s, tn, g.Nt, wt[i - nxy], wt[i], wt[i + nxy]);
+        acc_d1w(s, x, g.Nx, x > 0 ? WX[off - 1] : 0.0, WX[off], x < g.Nx - 1 ? WX[off + 1] : 0.0);
+        acc_d1w(s, y, g.Ny, y > 0 ? WY[off - g.Nx] : 0.0, WY[off], y < g.Ny - 1 ? WY[off + g.Nx] : 0.0);
+        const double bcm = E[2 * nxy + off], bcq = E[3 * nxy + off];
+        if (tn == 0) s -= (rho0[off] - bcm) + r * bcq;
+        if (tn == g.Nt - 1) s += (rhoT[off] - bcm) + r * bcq;
+        F[i] = s;
+        ff = s * s;
+    }
+    if (!gath_rr) return;
+    double v[1] = {ff}, tot[1];
+    if (grid_reduce_last<1>(v, rb, tot) && threadIdx.x == 0) gath_rr[0] += tot[0];
+}
+
+hipError_t launch_rhs_edge(const Geo& g, int n, const double* wt, const double* edge, const double* rho0,
+                           const double* rhoT, double r, double* F, RedBuf rb, double* gath_rr, hipStream_t s,
+                           const int* guard) {
+    if (n < 0 || n >= g.nloc) return hipErrorInvalidValue;
+    k_rhs_edge<<<flat_blocks(g.nxy), NT, 0, s>>>(g, n, wt, edge, rho0, rhoT, r, F, rb, gath_rr, guard);
     return hipGetLastError();
 }
 

@@ -373,19 +373,22 @@ def test_bb_fused_prox_rhs_chunks(gold, monkeypatch, tch, mode):
 @pytest.mark.parametrize("vr", [2, 3, 5])
 def test_bb_fused_prox_rhs_sharded(gold, monkeypatch, vr, mode, tch):
     """The fused prox + next RHS on time-slab shards (virtual ranks: the transfer lists RCCL
-    runs): a shard's first and last chunks recompute stepB on the neighbours' boundary planes
-    from a two-plane phi halo and a one-plane mu halo.  Textured golden, Nt = 5: at 5 ranks
-    every slab is one plane and its phi halo comes partly from two ranks away.  Against the
-    separate k_prox / k_rhs with their one-plane halos: mu, q, phi and the flow bit-identical in
-    the spectral modes; the stencil CG only rounds F.F differently."""
+    runs), both ways across a slab edge: deferred (default -- F of an edge plane finished by
+    k_rhs_edge after one w_t halo plane is exchanged; phi needs one halo plane) and recomputed
+    (FOTO_PR_EDGE=0 -- stepB on the neighbours' boundary planes from a two-plane phi halo and a
+    one-plane mu halo).  Textured golden, Nt = 5: at 5 ranks every slab is one plane (both edges
+    of it deferred; its recompute halo partly from two ranks away).  Against the separate k_prox /
+    k_rhs with their one-plane halos: mu, q, phi and the flow bit-identical in the spectral
+    modes; the stencil CG only rounds F.F differently."""
     if tch == "1" and mode != 2:
         pytest.skip("chunk seams inside shards: one mode suffices")
     d = gold("bb_tex.npz")
     Nt, Ny, Nx = (int(v) for v in d["shape"])
     r, _, eps, _ = d["params"]
     out = []
-    for env in ({"FOTO_FUSE_PR": "0"}, {"FOTO_FUSE_PR": "1"}):
-        monkeypatch.delenv("FOTO_PR_TCH", raising=False)
+    for env in ({"FOTO_FUSE_PR": "0"}, {"FOTO_FUSE_PR": "1"}, {"FOTO_FUSE_PR": "1", "FOTO_PR_EDGE": "0"}):
+        for k in ("FOTO_PR_TCH", "FOTO_PR_EDGE"):
+            monkeypatch.delenv(k, raising=False)
         if tch != "default":
             monkeypatch.setenv("FOTO_PR_TCH", tch)
         for k, v in env.items():
@@ -393,16 +396,17 @@ def test_bb_fused_prox_rhs_sharded(gold, monkeypatch, vr, mode, tch):
         with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps, cg_mode=mode, virtual_ranks=vr) as s:
             s.iterate(4, 0.0, False)
             out.append((s.state(), s.phi(), list(s.cg_its), np.array(s.crit), s.flow()))
+    monkeypatch.delenv("FOTO_PR_EDGE", raising=False)
     (mu0, q0), p0, c0, k0, f0 = out[0]
-    (mu1, q1), p1, c1, k1, f1 = out[1]
-    assert c0 == c1
-    np.testing.assert_allclose(k1, k0, rtol=1e-10 if mode == 0 else 1e-13, atol=0)
-    if mode != 0:
-        for x, y in ((mu0, mu1), (q0, q1), (p0, p1)) + tuple(zip(f0, f1)):
-            assert np.array_equal(x, y)
-    else:
-        for x, y in ((mu0, mu1), (q0, q1), (p0, p1)):
-            np.testing.assert_allclose(y, x, rtol=0, atol=1e-10 * max(np.abs(x).max(), 1e-300))
+    for (mu1, q1), p1, c1, k1, f1 in out[1:]:
+        assert c0 == c1
+        np.testing.assert_allclose(k1, k0, rtol=1e-10 if mode == 0 else 1e-13, atol=0)
+        if mode != 0:
+            for x, y in ((mu0, mu1), (q0, q1), (p0, p1)) + tuple(zip(f0, f1)):
+                assert np.array_equal(x, y)
+        else:
+            for x, y in ((mu0, mu1), (q0, q1), (p0, p1)):
+                np.testing.assert_allclose(y, x, rtol=0, atol=1e-10 * max(np.abs(x).max(), 1e-300))
 
 
 def test_bb_errors():

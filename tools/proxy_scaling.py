@@ -13,7 +13,8 @@ the curve is an upper bound on what W GPUs can reach.
 A communication MODEL is printed beside it (not a measurement: the RCCL calls have only run
 through the in-process transport): per rank and outer iteration the slab <-> row-box
 all-to-alls (each rank sends (W-1)/W of its slab each way, one peer per xGMI link), the
-two-plane phi and one-plane mu halos of the fused prox + RHS (both neighbours), the 32-KB
+one-plane phi and w_t halos of the fused prox + RHS with deferred slab edges (both
+neighbours; FOTO_PR_EDGE=0's recompute would send 2 phi + 3 mu planes), the 32-KB
 histogram all-gather and the crit all-gather, at LINK_GBS per direction per link and
 LAT_US per RCCL call.
 
@@ -45,7 +46,7 @@ def comm_model_us(W):
     a2a = nl * plane * (W - 1) / W            # bytes one rank sends in one all-to-all
     # W - 1 peers over 7 links (8 GPUs fully connected): a2a spread over min(W - 1, 7) links
     a2a_us = a2a / min(W - 1, 7) / (LINK_GBS * 1e3) + LAT_US
-    halo_us = (2 + 3) * plane / (LINK_GBS * 1e3) + LAT_US     # per neighbour: 2 phi + 3 mu planes
+    halo_us = 2 * plane / (LINK_GBS * 1e3) + 2 * LAT_US       # per neighbour: phi, then w_t, one plane each
     gath_us = 2 * LAT_US                                      # histogram (32 KB) + crit all-gathers
     parts = {"alltoall_x2": 2 * a2a_us, "halos": halo_us, "allgathers": gath_us}
     return sum(parts.values()), parts
@@ -104,7 +105,7 @@ def main():
                      f"{k.get('prox', 0) + k.get('rhs', 0):11.3f} {k.get('flow', 0) + k.get('other', 0):10.3f} "
                      f"{cm / 1e3:13.3f} {1e3 / model_ms:10.1f} {base / (r['W'] * model_ms):9.2f}")
     lines.append(f"# comm model: all-to-all bytes (W-1)/W of the rank's slab each way over min(W-1, 7) xGMI links, "
-                 f"halos 5 planes per neighbour, {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
+                 f"halos 2 planes per neighbour (phi, w_t), {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
                  f"(a model, not a measurement; no overlap with compute assumed).")
     lines.append("# cg: the CG kernels as timed by the library (mode 3: the Gauss-compressed CG's histogram and "
                  "node solve groups; mode 2: the s-step passes, incl. a deferred solve's no-op margin passes).")
