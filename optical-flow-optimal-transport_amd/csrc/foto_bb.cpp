@@ -198,6 +198,8 @@ struct foto_bb_ctx {
     hipEvent_t ph[2][4] = {};      // per slot: RHS start | CG start | prox start | crit readback
     hipEvent_t fl[2] = {};         // flow extraction
     double* hgath[2] = {nullptr, nullptr};   // pinned host mirrors of gath, per slot
+    double* dgath[2] = {nullptr, nullptr};   // their device addresses (coherent host memory)
+    bool hcrit = false;            // single shard, fused prox: the kernel writes crit to hgath itself
     int hpar = 0;                  // slot of the last head
     ~foto_bb_ctx() {
         if (s) (void)hipStreamSynchronize(s);   // (before the shards free their buffers)
@@ -286,7 +288,11 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     FOTO_TRY(stream_acquire(&c->s));
     FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hS, sizeof(CGScal)));
     const int W = c->W;
-    for (double*& h : c->hgath) FOTO_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(double) * 4 * W));
+    for (int k = 0; k < 2; ++k) {
+        FOTO_HIP_CHECK(hipHostMalloc((void**)&c->hgath[k], sizeof(double) * 4 * W,
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+        FOTO_HIP_CHECK(hipHostGetDevicePointer((void**)&c->dgath[k], c->hgath[k], 0));
+    }
     for (auto& p : c->ph)
         for (auto& e : p) FOTO_HIP_CHECK(hipEventCreate(&e));
     for (auto& e : c->fl) FOTO_HIP_CHECK(hipEventCreate(&e));
@@ -301,6 +307,10 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         c->fuse = !(e && atoi(e) == 0);
         const char* pe = getenv("FOTO_PIPE");   // 0: one outer iteration in flight (A/B runs)
         c->pipe = W == 1 && c->fuse && c->o.cg_mode == 3 && !(pe && atoi(pe) == 0);
+        // the crit readback as two stores of k_prox_rhs's last block into the slot (a copy launch
+        // on the stream costs ~4 us; FOTO_HOST_CRIT=0: the copy)
+        const char* hc = getenv("FOTO_HOST_CRIT");
+        c->hcrit = W == 1 && c->fuse && !(hc && atoi(hc) == 0);
     }
     for (int j = 0; j < nlocal; ++j) {
         auto sp = std::make_unique<Shard>();
@@ -574,8 +584,9 @@ static int outer_head(foto_bb_ctx* c) {
 // the fused k_prox_rhs of every local shard on the pair recorded in its fz_src -> fz_dst;
 // sharded: the two-plane phi halo and the one-plane halo of the mu it reads go first.
 // guarded: each shard's launch returns at once unless its CG's done flag is set.
-static int prox_rhs(foto_bb_ctx* c, bool guarded) {
+static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
     const int W = c->W;
+    double* hcrit = c->hcrit ? c->dgath[par] + 2 * W : nullptr;
     // sharded: defer the slab-edge F (default: two planes per neighbour on the wire, phi and w_t)
     // or recompute the neighbours' boundary stepB (FOTO_PR_EDGE=0: five planes, 2 phi + 3 mu)
     const char* pe = getenv("FOTO_PR_EDGE");
@@ -597,7 +608,7 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded) {
         FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.fz_dst[0], s.fz_dst[1],
                                        s.fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(W) + 2 * s.rank,
                                        c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s,
-                                       guarded ? s.spec->done_flag() : nullptr, dlo, dhi, s.wt, s.edge));
+                                       guarded ? s.spec->done_flag() : nullptr, dlo, dhi, s.wt, s.edge, hcrit));
         c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
     }
     if (defer) {
@@ -675,7 +686,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
         // (pipelined: mu -> nu -> xi -> mu rotate, so the mu before this iteration survives it)
         for (auto& sp : c->sh)
             for (int f = 0; f < 3; ++f) { sp->fz_src[f] = sp->mu[f]; sp->fz_dst[f] = sp->nu[f]; }
-        FOTO_TRY(prox_rhs(c, guarded));
+        FOTO_TRY(prox_rhs(c, guarded, e.par));
         for (auto& sp : c->sh)
             for (int f = 0; f < 3; ++f) {
                 if (c->pipe) {
@@ -700,7 +711,8 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
         }
     }
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
-    FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s0.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+    if (!c->hcrit)
+        FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s0.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
     FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
     e.dsp = dsp;
     e.sdefer = sdefer;
@@ -761,7 +773,7 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
             c->kt.discard_last(FOTO_K_PROX, 1);
             if (c->fuse) {
-                FOTO_TRY(prox_rhs(c, false));
+                FOTO_TRY(prox_rhs(c, false, e.par));
                 c->f_ready = true;   // (a rollback before the redo had cleared it)
             } else {
                 hipEvent_t t = c->kt.start(c->s);
@@ -769,7 +781,9 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
                                            s.rb, s.gath_crit(W), s.rank, c->s));
                 c->kt.stop(t, c->s, FOTO_K_PROX, 80.0 * nv);
             }
-            FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
+            if (!c->hcrit)
+                FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost,
+                                              c->s));
             FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
             FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
             c->st.cg_redo += 1;
@@ -789,7 +803,7 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             FOTO_TRY(sharded_sstep(c, cg_iters, cg_info));
             FOTO_TRY(sharded_inv(c));
             if (c->fuse) {
-                FOTO_TRY(prox_rhs(c, false));
+                FOTO_TRY(prox_rhs(c, false, e.par));
             } else {
                 FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
                 for (auto& sp : c->sh) {

@@ -226,7 +226,7 @@ hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, c
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s,
                            const int* guard = nullptr, int defer_lo = 0, int defer_hi = 0, double* wt_out = nullptr,
-                           double* edge = nullptr);
+                           double* edge = nullptr, double* hcrit = nullptr);
 // F of a deferred edge plane n (0 or nloc - 1; edge slot 0 or 1), F.F added to gath_rr[0]
 hipError_t launch_rhs_edge(const Geo& g, int n, const double* wt, const double* edge, const double* rho0,
                            const double* rhoT, double r, double* F, RedBuf rb, double* gath_rr, hipStream_t s,

@@ -754,7 +754,7 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         const double* __restrict__ muy, double* __restrict__ nut, double* __restrict__ nux, double* __restrict__ nuy,
         const double* __restrict__ rho0, const double* __restrict__ rhoT, double r, double inv_r,
         double* __restrict__ F, RedBuf rb, double* gath_crit, double* gath_rr, const int* __restrict__ guard, int tch,
-        int defer_lo, int defer_hi, double* __restrict__ wt_out, double* __restrict__ edge) {
+        int defer_lo, int defer_hi, double* __restrict__ wt_out, double* __restrict__ edge, double* hcrit) {
     if (guard && *guard == 0) return;
     __shared__ double fr[4][PR_FN];                  // phi ring (plane p in slot p & 3)
     __shared__ double wb[2][2][PR_PH * PR_PW];       // [plane & 1][x | y part] of w
@@ -942,6 +942,11 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         gath_crit[0] = tot[0];
         gath_crit[1] = tot[1];
         if (gath_rr) gath_rr[0] = tot[2];
+        if (hcrit) {   // (pinned, coherent host slot: the crit readback without a copy launch)
+            hcrit[0] = tot[0];
+            hcrit[1] = tot[1];
+            __threadfence_system();
+        }
     }
 }
 
@@ -962,16 +967,18 @@ int prox_rhs_blocks(const Geo& g) {
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard,
-                           int defer_lo, int defer_hi, double* wt_out, double* edge) {
+                           int defer_lo, int defer_hi, double* wt_out, double* edge, double* hcrit) {
     const int nb = prox_rhs_blocks(g);
     if (rb.cap < 3 * nb) return hipErrorInvalidValue;
     if ((defer_lo || defer_hi) && (!wt_out || !edge)) return hipErrorInvalidValue;
     if (defer_lo || defer_hi)
         k_prox_rhs<true><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
-                                              gath_crit, gath_rr, guard, prox_rhs_tch(g), defer_lo, defer_hi, wt_out, edge);
+                                              gath_crit, gath_rr, guard, prox_rhs_tch(g), defer_lo, defer_hi, wt_out, edge,
+                                              hcrit);
     else
         k_prox_rhs<false><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
-                                               gath_crit, gath_rr, guard, prox_rhs_tch(g), 0, 0, nullptr, nullptr);
+                                               gath_crit, gath_rr, guard, prox_rhs_tch(g), 0, 0, nullptr, nullptr,
+                                               hcrit);
     return hipGetLastError();
 }
 

@@ -2796,6 +2796,7 @@ struct SpecImpl {
     GqState* gq = nullptr;
     GqState* hgq2[2] = {nullptr, nullptr};   // pinned: the header (K, status, conv, done, bn2, rn2) of
     int hslot = 0, hlast = 0;                // the last two solves (hslot: the next one's)
+    GqState* dgq2[2] = {nullptr, nullptr};   // their device addresses (coherent host memory)
     GqNodes* gqn = nullptr;
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
     double* gq_tab = nullptr;
@@ -3022,9 +3023,10 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     if (P->gauss) {
         FOTO_TRY(P->alloc(sizeof(GqState), &b)); P->gq = (GqState*)b;
         FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
-        for (GqState*& h : P->hgq2) {
-            FOTO_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(GqState)));
-            std::memset((void*)h, 0, sizeof(GqState));
+        for (int k = 0; k < 2; ++k) {
+            FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hgq2[k], sizeof(GqState), hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset((void*)P->hgq2[k], 0, sizeof(GqState));
+            FOTO_HIP_CHECK(hipHostGetDevicePointer((void**)&P->dgq2[k], P->hgq2[k], 0));
         }
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
@@ -3373,14 +3375,18 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
     FOTO_HIP_CHECK(hipGetLastError());
     const char* kl = getenv("FOTO_GQ_KLIM");   // (tests: force the s-step redo path)
     const int klim = kl ? std::max(0, std::min(GQ_KMAX, atoi(kl))) : GQ_KMAX;
-    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq);
+    // the header to the host slot: stored by the CG kernel itself (FOTO_HOST_CRIT=0: a copy)
+    P->hlast = P->hslot;
+    P->hslot ^= 1;
+    const char* hc = getenv("FOTO_HOST_CRIT");
+    const bool direct = !(hc && atoi(hc) == 0);
+    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq, direct ? P->dgq2[P->hlast] : nullptr);
     FOTO_HIP_CHECK(hipGetLastError());
     k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->r * P->eps, P->c1, P->gq_tab);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
-    P->hlast = P->hslot;
-    P->hslot ^= 1;
-    FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq2[P->hlast], P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
+    if (!direct)
+        FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq2[P->hlast], P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
     P->gauss_active = true;
     return 0;
 }

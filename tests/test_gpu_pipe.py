@@ -20,7 +20,7 @@ from foto.bb import BBSolver  # noqa: E402
 
 
 def _run(d, monkeypatch, env, calls, **kw):
-    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM", "FOTO_CG_DEFER"):
+    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM", "FOTO_CG_DEFER", "FOTO_HOST_CRIT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -123,4 +123,19 @@ def test_sharded_gauss_deferred(gold, monkeypatch, vr, klim):
     if klim == "1":
         assert a["stats"]["cg_redo"] == n
     assert np.max(np.abs(a["its"] - d["cg_its"])) <= 1
+    np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("klim", [None, "200"])
+def test_host_readback_stores(gold, monkeypatch, klim):
+    """The crit pair and the Gauss solve's header reach the host as stores of the kernels
+    themselves into pinned, coherent slots (no copy launch); FOTO_HOST_CRIT=0 copies them on the
+    stream instead.  Same run either way, including the redone solves (KLIM 200)."""
+    d = gold("bb_c1.npz")
+    max_it = int(d["params"][3])
+    env = {} if klim is None else {"FOTO_GQ_KLIM": klim}
+    a = _run(d, monkeypatch, env, [(max_it, None, True)])
+    b = _run(d, monkeypatch, {**env, "FOTO_HOST_CRIT": "0"}, [(max_it, None, True)])
+    _same(a, b)
+    assert a["stats"]["cg_redo"] == b["stats"]["cg_redo"]
     np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)

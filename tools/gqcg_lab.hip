@@ -257,7 +257,7 @@ int main(int argc, char** argv) {
         printf("%-28s %8.2f us/solve  %6.3f us/step  K %d status %d  max rel d(alpha,beta) %.2e\n", name,
                1e3 * ms / reps, 1e3 * ms / reps / maxiter, K, st, err);
     };
-    timeit("product k_gq_cg (256)", [&] { k_gq_cg<<<1, GQ_CGNTH>>>(nd, 0.0, maxiter, GQ_KMAX, S0); }, false);
+    timeit("product k_gq_cg (256)", [&] { k_gq_cg<<<1, GQ_CGNTH>>>(nd, 0.0, maxiter, GQ_KMAX, S0, nullptr); }, false);
     CK(hipMemcpy(&h0, S0, sizeof(GqState), hipMemcpyDeviceToHost));
     printf("  product: K %d status %d rn2/bn2 %.3e\n", h0.K, h0.status, h0.rn2 / h0.bn2);
     timeit("lr/ap 64 (one wave)", [&] { k_cg_var<64, 0><<<1, 64>>>(nd, 0.0, maxiter, S1); }, true);
