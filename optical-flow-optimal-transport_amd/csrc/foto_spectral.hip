@@ -2807,7 +2807,7 @@ struct SpecImpl {
     int gq_nch = 0;
     int* gq_cfirst = nullptr;     // [GQ_NB + 1] first chunk of each bin
     double* gq_rowmu = nullptr;   // mu_t + mu_y per box row
-    double* gq_ppart = nullptr;   // [gq_nch][GQ_NM] chunk sums
+    double* gq_ppart = nullptr;   // [chunk id][GQ_NM] chunk sums
     GqExact* gq_exact = nullptr;  // exact bins (the whole grid's distinct eigenvalues)
 
     // k_spec_s2r LATE: working ring passes plan at their start (single shard unless split;
@@ -3089,6 +3089,60 @@ static int gq_perm_lists(SpecImpl* P, const SpecTab& T, unsigned* perm, double* 
     return rc ? -1 : 0;
 }
 
+// The chunk list in dispatch order.  Neighbouring bins share the cache lines of b^ (a 16-voxel
+// line holds runs of ~2 bins of a row), and a bin's chunks walk the rows in order, so the chunks
+// of all bins over the same rows read the same lines at about the same time -- from the same L2
+// only if they run on the same XCD.  Workgroups go round-robin to the 8 XCDs (block k to XCD
+// k % 8) and a block's 4 waves take slots 4k .. 4k + 3: slot lists are filled so that XCD x
+// gets the chunks whose first row lies in the x-th eighth of the rows (FOTO_GQ_XCD=0: bin order).
+// The sums go to part[chunk id] either way, so the histogram is bit-identical.
+static int gq_order_chunks(SpecImpl* P, std::vector<GqChunk>& ch, int rows, hipStream_t s) {
+    const char* e = getenv("FOTO_GQ_XCD");
+    const int nx = 8;
+    const int n = (int)ch.size();
+    if ((e && atoi(e) == 0) || n < 4 * nx) return 0;
+    void* b = nullptr;
+    GqChunk* dch = nullptr;
+    int* drow = nullptr;
+    FOTO_HIP_CHECK(hipMalloc(&b, sizeof(GqChunk) * n + sizeof(int) * n));
+    dch = (GqChunk*)b;
+    drow = (int*)(dch + n);
+    std::vector<int> row(n);
+    int rc = 0;
+    if (hipMemcpyAsync(dch, ch.data(), sizeof(GqChunk) * n, hipMemcpyHostToDevice, s) != hipSuccess) rc = -1;
+    if (!rc) {
+        k_gq_chunk_rows<<<(n + 255) / 256, 256, 0, s>>>(dch, n, P->gq_permv, drow);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(row.data(), drow, sizeof(int) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = -1;
+    }
+    (void)hipFree(b);
+    if (rc) {
+        set_error("gauss chunk order: device step failed");
+        return FOTO_ERR_HIP;
+    }
+    std::vector<std::vector<int>> L(nx);
+    for (int c = 0; c < n; ++c) L[std::min(nx - 1, (int)((int64_t)row[c] * nx / std::max(1, rows)))].push_back(c);
+    std::vector<size_t> at(nx, 0);
+    const int nb = (n + 3) / 4;
+    std::vector<GqChunk> out((size_t)nb * 4, GqChunk{0, 0, 0, -1});
+    for (int k = 0; k < nb; ++k)
+        for (int w = 0; w < 4; ++w) {
+            int x = k % nx;
+            if (at[x] == L[x].size()) {   // this XCD's share is used up: the longest remaining list
+                size_t best = 0;
+                x = -1;
+                for (int y = 0; y < nx; ++y)
+                    if (L[y].size() - at[y] > best) { best = L[y].size() - at[y]; x = y; }
+                if (x < 0) continue;
+            }
+            out[(size_t)k * 4 + w] = ch[L[x][at[x]++]];
+        }
+    ch.swap(out);
+    return 0;
+}
+
 // this box's list and chunks, and the exact bins of the whole grid (from the box's list when the
 // box is the grid, else from a scratch list of the grid: every rank derives the same table)
 static int gq_build_perm(SpecImpl* P, hipStream_t s) {
@@ -3114,13 +3168,15 @@ static int gq_build_perm(SpecImpl* P, hipStream_t s) {
     for (int bb = 0; bb < GQ_NB; ++bb) {
         cfirst[bb] = (int)ch.size();
         for (int st = 0; st < htot[bb]; st += GQ_PCH)
-            ch.push_back(GqChunk{bb, hfirst[bb] + st, std::min(GQ_PCH, htot[bb] - st), 0});
+            ch.push_back(GqChunk{bb, hfirst[bb] + st, std::min(GQ_PCH, htot[bb] - st), (int)ch.size()});
     }
     cfirst[GQ_NB] = (int)ch.size();
+    const int nch = (int)ch.size();
+    FOTO_TRY(P->alloc(sizeof(int) * (GQ_NB + 1), &b)); P->gq_cfirst = (int*)b;
+    FOTO_TRY(P->alloc(sizeof(double) * GQ_NM * std::max(1, nch), &b)); P->gq_ppart = (double*)b;
+    FOTO_TRY(gq_order_chunks(P, ch, rows, s));
     P->gq_nch = (int)ch.size();
     FOTO_TRY(P->alloc(sizeof(GqChunk) * std::max<size_t>(1, ch.size()), &b)); P->gq_chunks = (GqChunk*)b;
-    FOTO_TRY(P->alloc(sizeof(int) * (GQ_NB + 1), &b)); P->gq_cfirst = (int*)b;
-    FOTO_TRY(P->alloc(sizeof(double) * GQ_NM * std::max<size_t>(1, ch.size()), &b)); P->gq_ppart = (double*)b;
     FOTO_HIP_CHECK(hipMemcpyAsync(P->gq_chunks, ch.data(), sizeof(GqChunk) * ch.size(), hipMemcpyHostToDevice, s));
     FOTO_HIP_CHECK(hipMemcpyAsync(P->gq_cfirst, cfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice, s));
     if (P->nyl == P->g.Ny) {
