@@ -97,7 +97,8 @@ typedef struct {
     int outer_iters;          /* outer iterations completed so far                      */
     int64_t cg_iters_total;   /* CG iterations over all outer iterations                */
     double last_crit;
-    double ms_rhs, ms_cg, ms_prox, ms_flow;   /* phase wall time (HIP events)           */
+    double ms_rhs, ms_cg, ms_prox, ms_flow;   /* phase wall time (HIP events; RHS / CG / prox
+                                                 only with timing = 1)                   */
     /* per kernel class (timing = 1): launches and summed device time in ms            */
     int64_t n_k[8];
     double ms_k[8];

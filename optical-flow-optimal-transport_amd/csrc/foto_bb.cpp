@@ -189,6 +189,7 @@ struct foto_bb_ctx {
         double* fz_dst[3];
         bool f_ready;
         int hpar;
+        bool pev;                      // phase events recorded (ph[par][0..3])
     };
     std::vector<Enq> inflight;   // oldest first
     // bookkeeping
@@ -196,10 +197,12 @@ struct foto_bb_ctx {
     foto_bb_stats st{};
     KTimer kt;
     hipEvent_t ph[2][4] = {};      // per slot: RHS start | CG start | prox start | crit readback
+    hipEvent_t fin[2] = {};        // per slot: crit readback without timing (phase events off)
     hipEvent_t fl[2] = {};         // flow extraction
     double* hgath[2] = {nullptr, nullptr};   // pinned host mirrors of gath, per slot
     double* dgath[2] = {nullptr, nullptr};   // their device addresses (coherent host memory)
     bool hcrit = false;            // single shard, fused prox: the kernel writes crit to hgath itself
+    bool phase_force = false;      // FOTO_PHASE_EV=1: phase events even without kernel timing
     int hpar = 0;                  // slot of the last head
     ~foto_bb_ctx() {
         if (s) (void)hipStreamSynchronize(s);   // (before the shards free their buffers)
@@ -210,6 +213,7 @@ struct foto_bb_ctx {
         for (auto& p : ph)
             for (auto e : p) if (e) (void)hipEventDestroy(e);
         for (auto e : fl) if (e) (void)hipEventDestroy(e);
+        for (auto e : fin) if (e) (void)hipEventDestroy(e);
         if (s) {
             (void)hipStreamSynchronize(s);
             stream_release(s);
@@ -296,6 +300,7 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     for (auto& p : c->ph)
         for (auto& e : p) FOTO_HIP_CHECK(hipEventCreate(&e));
     for (auto& e : c->fl) FOTO_HIP_CHECK(hipEventCreate(&e));
+    for (auto& e : c->fin) FOTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (c->rccl) {
         ncclUniqueId id;
         memcpy(&id, c->o.nccl_id, sizeof(id));
@@ -309,6 +314,11 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         c->pipe = W == 1 && c->fuse && c->o.cg_mode == 3 && !(pe && atoi(pe) == 0);
         // the crit readback as two stores of k_prox_rhs's last block into the slot (a copy launch
         // on the stream costs ~4 us; FOTO_HOST_CRIT=0: the copy)
+        // phase events (the RHS / CG / prox split of foto_bb_stats) only with kernel timing on:
+        // three timed event records per outer iteration cost ~13 us of GPU time at the bench
+        // grid (1561-1572 vs 1603-1616 it/s, same box), and the crit sync uses a timing-free one
+        const char* pv = getenv("FOTO_PHASE_EV");
+        c->phase_force = pv && atoi(pv) == 1;
         const char* hc = getenv("FOTO_HOST_CRIT");
         c->hcrit = W == 1 && c->fuse && !(hc && atoi(hc) == 0);
     }
@@ -561,9 +571,11 @@ static int cg_solve(foto_bb_ctx* c, int* iters, int* info) {
 // iteration's crit (the stop rules can still end the run there: F is scratch; a CG redo re-runs
 // the head).  With two in flight (c->pipe) the whole next iteration is enqueued first.  The
 // host callback runs after the next iteration is enqueued.
+static bool phase_on(const foto_bb_ctx* c) { return c->phase_force || c->kt.on; }
+
 static int outer_head(foto_bb_ctx* c) {
     c->hpar ^= 1;
-    FOTO_HIP_CHECK(hipEventRecord(c->ph[c->hpar][0], c->s));
+    if (phase_on(c)) FOTO_HIP_CHECK(hipEventRecord(c->ph[c->hpar][0], c->s));
     // the previous iteration's k_prox_rhs wrote F (and F.F).  (Enqueuing the next solve's x-DCT
     // here, ahead of the crit wait, measured no faster: 457 vs 457 it/s same box.)
     if (c->fuse && c->f_ready) return 0;
@@ -646,9 +658,10 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     e.f_ready = c->f_ready;
     e.hpar = c->hpar ^ 1;   // (before this iteration's head)
     hipEvent_t* ph = c->ph[e.par];
+    e.pev = phase_on(c);
     // phase boundaries are recorded, not waited on: the one host wait per outer iteration
     // is the crit readback below (a wait here idled the GPU for the host's wake-up)
-    FOTO_HIP_CHECK(hipEventRecord(ph[1], c->s));
+    if (e.pev) FOTO_HIP_CHECK(hipEventRecord(ph[1], c->s));
     // Single shard, spectral: the solve is enqueued without a host wait and prox follows behind
     // it, guarded by the CG's done flag; the one sync (crit) then also delivers the CG result.
     // A solve that needs more work (s-step: more passes than predicted; Gauss: K beyond the
@@ -678,7 +691,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
         FOTO_TRY(cg_solve(c, &e.its, &e.info));
     }
     const bool guarded = dsp != nullptr || sdefer;
-    FOTO_HIP_CHECK(hipEventRecord(ph[2], c->s));
+    if (e.pev) FOTO_HIP_CHECK(hipEventRecord(ph[2], c->s));
     c->have_phi = 1;
 
     if (c->fuse) {
@@ -713,7 +726,7 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
     FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
     if (!c->hcrit)
         FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s0.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost, c->s));
-    FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
+    FOTO_HIP_CHECK(hipEventRecord(e.pev ? ph[3] : c->fin[e.par], c->s));
     e.dsp = dsp;
     e.sdefer = sdefer;
     c->inflight.push_back(e);
@@ -760,7 +773,8 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
     *cg_iters = e.its;
     *cg_info = e.info;
     hipEvent_t* ph = c->ph[e.par];
-    FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
+    const hipEvent_t done = e.pev ? ph[3] : c->fin[e.par];   // the crit readback
+    FOTO_HIP_CHECK(hipEventSynchronize(done));
     if (dsp) {
         // a failed solve is redone once the iteration behind it (whose prox its done-flag chain
         // skipped) is dropped; the loop enqueues that iteration again
@@ -784,8 +798,8 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             if (!c->hcrit)
                 FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], s.gath, sizeof(double) * 4 * W, hipMemcpyDeviceToHost,
                                               c->s));
-            FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
-            FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
+            FOTO_HIP_CHECK(hipEventRecord(done, c->s));
+            FOTO_HIP_CHECK(hipEventSynchronize(done));
             c->st.cg_redo += 1;
         }
     }
@@ -815,16 +829,18 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             FOTO_TRY(allgather(c, [W](Shard& s) { return s.gath_crit(W); }, 2));
             FOTO_HIP_CHECK(hipMemcpyAsync(c->hgath[e.par], c->sh[0]->gath, sizeof(double) * 4 * W,
                                           hipMemcpyDeviceToHost, c->s));
-            FOTO_HIP_CHECK(hipEventRecord(ph[3], c->s));
-            FOTO_HIP_CHECK(hipEventSynchronize(ph[3]));
+            FOTO_HIP_CHECK(hipEventRecord(done, c->s));
+            FOTO_HIP_CHECK(hipEventSynchronize(done));
             c->st.cg_redo += 1;
         }
         c->last_cg = *cg_iters;
     }
     float t_rhs = 0.f, t_cg = 0.f, t_prox = 0.f;
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, ph[0], ph[1]));
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, ph[1], ph[2]));
-    FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, ph[2], ph[3]));
+    if (e.pev) {
+        FOTO_HIP_CHECK(hipEventElapsedTime(&t_rhs, ph[0], ph[1]));
+        FOTO_HIP_CHECK(hipEventElapsedTime(&t_cg, ph[1], ph[2]));
+        FOTO_HIP_CHECK(hipEventElapsedTime(&t_prox, ph[2], ph[3]));
+    }
     c->st.ms_rhs += t_rhs;
     c->st.ms_cg += t_cg;
     c->st.ms_prox += t_prox;

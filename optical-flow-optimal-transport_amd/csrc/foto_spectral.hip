@@ -2462,6 +2462,26 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
     constexpr int H = TCol<NTT>::H;
     const int64_t ncols = (int64_t)T.nyl * T.Nx;
     const int64_t c = (int64_t)blockIdx.x * TC_NTH + threadIdx.x;
+    if constexpr (MODE == TC_PLAIN) {
+        // b^ only: the whole column's loads first (no mu_t staging, no barrier: with them the
+        // column loads started a memory latency late and were waited for in pieces)
+        if (c >= ncols) return;
+        double x[NTT];
+#pragma unroll
+        for (int j = 0; j < NTT; ++j) x[j] = in[j * ncols + c];
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            double e = 0.0, o = 0.0;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                e = fma(Ch[m * H + j], x[j] + x[NTT - 1 - j], e);
+                o = fma(Ch[H * H + m * H + j], x[j] - x[NTT - 1 - j], o);
+            }
+            bh[(2 * m) * ncols + c] = e;
+            bh[(2 * m + 1) * ncols + c] = o;
+        }
+        return;
+    }
     const SStep S0 = *Sg;
     const double c0 = S0.ic0, ic1 = 1.0 / S0.ic1;   // INIT interval (previous solve's b^ measure)
     double acc[NMOM];

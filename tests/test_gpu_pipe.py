@@ -20,7 +20,7 @@ from foto.bb import BBSolver  # noqa: E402
 
 
 def _run(d, monkeypatch, env, calls, **kw):
-    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM", "FOTO_CG_DEFER", "FOTO_HOST_CRIT"):
+    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM", "FOTO_CG_DEFER", "FOTO_HOST_CRIT", "FOTO_PHASE_EV"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -138,4 +138,20 @@ def test_host_readback_stores(gold, monkeypatch, klim):
     b = _run(d, monkeypatch, {**env, "FOTO_HOST_CRIT": "0"}, [(max_it, None, True)])
     _same(a, b)
     assert a["stats"]["cg_redo"] == b["stats"]["cg_redo"]
+    np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("klim", [None, "200"])
+def test_phase_events_only_with_timing(gold, monkeypatch, klim):
+    """The RHS / CG / prox phase events are recorded only with kernel timing on (or
+    FOTO_PHASE_EV=1); the crit sync then uses a timing-free event.  Same run either way,
+    including the redone solves (KLIM 200); the phase times are 0 without the events."""
+    d = gold("bb_c1.npz")
+    max_it = int(d["params"][3])
+    env = {} if klim is None else {"FOTO_GQ_KLIM": klim}
+    a = _run(d, monkeypatch, env, [(max_it, None, True)])
+    c = _run(d, monkeypatch, {**env, "FOTO_PHASE_EV": "1"}, [(max_it, None, True)])
+    _same(a, c)
+    assert a["stats"]["cg_redo"] == c["stats"]["cg_redo"]
+    assert c["stats"]["ms_cg"] > 0 and a["stats"]["ms_cg"] == 0
     np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)
