@@ -298,9 +298,9 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         FOTO_HIP_CHECK(hipHostGetDevicePointer((void**)&c->dgath[k], c->hgath[k], 0));
     }
     for (auto& p : c->ph)
-        for (auto& e : p) FOTO_HIP_CHECK(hipEventCreate(&e));
+        for (int k = 0; k < 4; ++k)   // (phase boundaries: timing only; the crit event keeps the fence)
+            FOTO_HIP_CHECK(hipEventCreateWithFlags(&p[k], k < 3 ? hipEventDisableSystemFence : hipEventDefault));
     for (auto& e : c->fl) FOTO_HIP_CHECK(hipEventCreate(&e));
-    for (auto& e : c->fin) FOTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (c->rccl) {
         ncclUniqueId id;
         memcpy(&id, c->o.nccl_id, sizeof(id));
@@ -321,6 +321,13 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         c->phase_force = pv && atoi(pv) == 1;
         const char* hc = getenv("FOTO_HOST_CRIT");
         c->hcrit = W == 1 && c->fuse && !(hc && atoi(hc) == 0);
+        // the crit sync: with the crit pair and the Gauss header stored into coherent host memory
+        // by the kernels themselves (fenced there), the event needs no system-scope fence of its
+        // own -- a fenced record writes the L2's dirty lines back once per outer iteration
+        // (FOTO_SYNC_FENCE=1: fenced)
+        const char* sf = getenv("FOTO_SYNC_FENCE");
+        const unsigned ff = (c->hcrit && !(sf && atoi(sf) == 1)) ? hipEventDisableSystemFence : 0u;
+        for (auto& e : c->fin) FOTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | ff));
     }
     for (int j = 0; j < nlocal; ++j) {
         auto sp = std::make_unique<Shard>();

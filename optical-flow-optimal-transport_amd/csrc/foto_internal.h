@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -90,8 +91,16 @@ struct KTimer {
 
     hipEvent_t get() {
         if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        // timing only, no system-scope fence: a fenced record writes the L2's dirty lines back
+        // before the next launch, which the untimed loop never does -- the launch after it then
+        // ran on a clean L2 (k_prox_rhs 171 us against 179.5 in the loop; FOTO_KT_FENCE=1: fenced)
+        static const bool fence = [] {
+            const char* f = getenv("FOTO_KT_FENCE");
+            return f && atoi(f) == 1;
+        }();
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, fence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess)
+            return nullptr;
         return e;
     }
     // returns the start event to be paired by stop()

@@ -15,5 +15,10 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/prof_fetch -o run --
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/prof_write -o run -- python3 bench.py $args --no-kernel-timing > $O/prof_write.log 2>&1 || exit $?
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/cal_fetch -o run -- tools/calib_fetch > $O/cal_fetch.log 2>&1 || exit $?
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/cal_write -o run -- tools/calib_fetch > $O/cal_write.log 2>&1 || exit $?
+# the bench command itself (timed loop + kernel-timing pass) under the kernel trace: the dominant
+# kernel's launches of each segment (tools/prox_segments.py)
+rm -rf $O/prof_kt2
+timeout -k 10 240 rocprofv3 --kernel-trace -f csv -d $O/prof_kt2 -o run -- python3 bench.py $args > $O/prof_kt2.log 2>&1 || exit $?
+python3 tools/prox_segments.py $O/prof_kt2/run_kernel_trace.csv 10 2 > $O/prox_segments.txt || exit $?
 python3 tools/summarize_profile.py --tag "$tag" --kt $O/prof_kt --fetch $O/prof_fetch --write $O/prof_write \
     --calib-fetch $O/cal_fetch --calib-write $O/cal_write --bench $O/bench_full.log --out $O/profiles_new
