@@ -3369,13 +3369,23 @@ static hipError_t launch_xhat(SpecImpl* P, hipStream_t s) {
 
 // plan (forward): single shard, the kernel plans the first pass; sharded, it leaves this rank's INIT
 // moments in gath for the all-gather
-// x^ = Q(lam) b^ (the Gauss-compressed CG's solution table) into a box buffer: one persistent
-// 1024-thread block per CU (the 128 KB half-bin table allows one)
+// x^ = Q(lam) b^ (the Gauss-compressed CG's solution table) into a box buffer: persistent
+// 1024-thread blocks, the table in LDS.  Sized for the whole table (32 rows, 128 KB) one block
+// fits a CU; sized for the first FOTO_GQ_XQL rows (default 17: 68 KB, what K <= ~200 needs;
+// the table kernel's qn is not known when this launch is enqueued) two fit, and any rows beyond
+// are read from the global table.  (FOTO_GQ_XQL=0: the whole table, one block per CU.)
 static hipError_t gq_xhat(SpecImpl* P, double* out, hipStream_t s) {
     const SpecTab T = P->tab();
     const int rows = P->g.Nt * P->nyl;
-    const int nb = std::max(1, std::min(cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
-    k_gq_xhat<<<nb, GQ_XNTH, GQ_TAB_BYTES, s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins, 1.0 / P->c1, out);
+    static const int xql = [] {
+        const char* e = getenv("FOTO_GQ_XQL");
+        return e ? atoi(e) : 17;
+    }();
+    const int ql = (xql > 0 && xql < GQ_QN) ? xql : GQ_QN;
+    const int per_cu = (ql < GQ_QN) ? 2 : 1;
+    const int nb = std::max(1, std::min(per_cu * cus_count(), (rows + GQ_XNTH / 64 - 1) / (GQ_XNTH / 64)));
+    k_gq_xhat<<<nb, GQ_XNTH, (size_t)ql * GQ_QB * sizeof(double), s>>>(T, P->bh, P->gq_tab, P->gq, P->gq_bins,
+                                                                       1.0 / P->c1, out, ql);
     return hipGetLastError();
 }
 
