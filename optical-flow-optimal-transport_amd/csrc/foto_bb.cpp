@@ -437,8 +437,10 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
 
 // all-to-all between the physical slabs and the spectral row boxes (foto_xfer.h)
 static int alltoall_spec(foto_bb_ctx* c, bool forward) {
-    auto sbuf = [&](Shard& s) { return forward ? s.spec->stage() : s.spec->box_out(); };
-    auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.spec->stage(); };
+    // the slab side is the shard's RHS buffer: fwd_local leaves the x / y DCTs of F there, and
+    // inv_local takes the inverse's slab from it (F is consumed by then)
+    auto sbuf = [&](Shard& s) { return forward ? s.rv : s.spec->box_out(); };
+    auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.rv; };
     return exchange(c, alltoall_xfers(c->Nt, c->Ny, c->Nx, c->W, forward), sbuf, rbuf);
 }
 

@@ -37,7 +37,6 @@ struct SpectralPlan {
     int poll(int* done, int* iters, int* passes, hipStream_t s);
     int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
     int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // unpack stage, inverse y, x
-    double* stage() const;     // physical-side all-to-all buffer [h][tl][rows of h][x]
     double* box_in() const;    // box-side receive buffer [t][rows][x]
     double* box_out() const;   // box-side send buffer of the inverse
     double* gath() const;      // world * moments() doubles

@@ -2738,35 +2738,6 @@ static bool tpair_size(int n) {
     return false;
 }
 
-// balanced contiguous split of n items over W parts (csrc/foto_bb.cpp split_planes)
-__device__ __forceinline__ int split_owner(int n, int W, int i) {
-    const int base = n / W, extra = n % W;
-    const int big = extra * (base + 1);
-    return (i < big) ? i / (base + 1) : extra + (i - big) / base;
-}
-__device__ __forceinline__ int split_start(int n, int W, int h) {
-    const int base = n / W, extra = n % W;
-    return h * base + (h < extra ? h : extra);
-}
-
-// own slab planes [tl][y][x] <-> all-to-all staging [h][tl][y - y0_h][x] (rows of peer h)
-template <bool PACK>
-__global__ __launch_bounds__(NT) void k_spec_pack(int nloc, int Ny, int Nx, int W, double* __restrict__ planes,
-                                                  double* __restrict__ stage) {
-    const int64_t n = (int64_t)nloc * Ny * Nx;
-    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-        const int64_t plane = (int64_t)Ny * Nx;
-        const int tl = (int)(i / plane);
-        const int64_t rem = i - tl * plane;
-        const int y = (int)(rem / Nx), x = (int)(rem - (int64_t)y * Nx);
-        const int h = split_owner(Ny, W, y);
-        const int y0h = split_start(Ny, W, h), nyh = split_start(Ny, W, h + 1) - y0h;
-        const int64_t j = (int64_t)nloc * Nx * y0h + ((int64_t)tl * nyh + (y - y0h)) * Nx + x;
-        if (PACK) stage[j] = planes[i];
-        else planes[i] = stage[j];
-    }
-}
-
 // ============================================================================ plan
 
 static int split_start_h(int n, int W, int h) {
@@ -2780,7 +2751,7 @@ struct SpecImpl {
     int y0 = 0, nyl = 0;          // spectral box rows (sharded: Ny split over ranks)
     double r = 1, eps = 0;
     double *bh = nullptr, *rh = nullptr, *ph = nullptr, *tmp = nullptr;   // spectral box
-    double *tmpp = nullptr, *stage = nullptr;                               // physical slab scratch
+    double* tmpp = nullptr;                                                 // physical slab scratch
     double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
     double *mx = nullptr, *my = nullptr, *mt = nullptr;
     double *Fx = nullptr, *Fy = nullptr, *Ft = nullptr;   // FFT-DCT tables (nullptr: GEMM path)
@@ -2938,7 +2909,6 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     FOTO_TRY(P->alloc(std::max(NB, NS) * 8, &b)); P->tmp = (double*)b;
     if (world > 1) {
         FOTO_TRY(P->alloc(NS * 8, &b)); P->tmpp = (double*)b;
-        FOTO_TRY(P->alloc(NS * 8, &b)); P->stage = (double*)b;
     }
     std::vector<double> C, CT, mu;
     if (g_dct_fft < 0) {
@@ -3730,12 +3700,9 @@ int SpectralPlan::fwd_local(double* b, KTimer* kt, hipStream_t s) {
     const Geo& g = P->g;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
     FOTO_HIP_CHECK(dct_pass(P, 0, false, g.nloc * g.Ny, 1, b, P->tmpp, s));      // x
-    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.nloc, g.Nx, P->tmpp, b, s));          // y
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.nloc, g.Nx, P->tmpp, b, s));          // y (b: the all-to-all's source)
     const int64_t n = (int64_t)g.nloc * g.nxy;
-    k_spec_pack<true><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world, b,
-                                                                                     P->stage);
-    FOTO_HIP_CHECK(hipGetLastError());
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 4.0 * 8.0 * (double)n);
     return 0;
 }
 
@@ -3811,12 +3778,9 @@ int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t 
     const Geo& g = P->g;
     const int64_t n = (int64_t)g.nloc * g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_spec_pack<false><<<(int)std::min<int64_t>((n + NT - 1) / NT, 8192), NT, 0, s>>>(g.nloc, g.Ny, g.Nx, P->world,
-                                                                                      scratch, P->stage);
-    FOTO_HIP_CHECK(hipGetLastError());
-    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.nloc, g.Nx, scratch, P->tmpp, s));     // y
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.nloc, g.Nx, scratch, P->tmpp, s));     // y (scratch: the all-to-all's target)
     FOTO_HIP_CHECK(dct_pass(P, 0, true, g.nloc * g.Ny, 1, P->tmpp, x, s));       // x
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * (double)n);
+    if (kt) kt->stop(e, s, FOTO_K_DCT, 4.0 * 8.0 * (double)n);
     return 0;
 }
 
@@ -3864,7 +3828,6 @@ int SpectralPlan::reset(hipStream_t s) {
     return reset_s2(P, s);
 }
 
-double* SpectralPlan::stage() const { return ((SpecImpl*)impl)->stage; }
 double* SpectralPlan::box_in() const { return ((SpecImpl*)impl)->tmp; }
 double* SpectralPlan::box_out() const {
     const SpecImpl* P = (const SpecImpl*)impl;

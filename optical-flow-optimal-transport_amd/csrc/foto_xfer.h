@@ -64,11 +64,14 @@ inline std::vector<Xfer> halo_depth_xfers(int Nt, int64_t nxy, int W, int depth)
     return xs;
 }
 
-// all-to-all between the physical slabs and the spectral row boxes (SpectralPlan):
-//   forward : rank a sends stage_a[na*Nx*y0_b, + na*nyl_b*Nx]   -> box_in_b[t0_a*nyl_b*Nx, ...]
-//   backward: rank a sends box_out_a[t0_b*nyl_a*Nx, + nb*nyl_a*Nx] -> stage_b[nb*Nx*y0_a, ...]
+// all-to-all between the physical slabs and the spectral row boxes (SpectralPlan), one transfer
+// per (source, destination, plane) straight between the natural layouts -- no packing pass:
+//   forward : rank a's slab [tl][y][x], rows [y0_b, + nyl_b) of its plane tl -> box_in_b[t0_a + tl][.][.]
+//   backward: rank a's box_out [t][y - y0_a][x], plane t0_b + tl             -> slab_b[tl][y0_a ..][.]
+// (a plane's rows of one box are contiguous on both sides: nyl * Nx doubles per transfer)
 inline std::vector<Xfer> alltoall_xfers(int Nt, int Ny, int Nx, int W, bool forward) {
     std::vector<Xfer> xs;
+    const int64_t nxy = (int64_t)Nx * Ny;
     for (int a = 0; a < W; ++a)
         for (int b = 0; b < W; ++b) {
             int ta, na, tb, nb, ya, nya, yb, nyb;
@@ -76,13 +79,17 @@ inline std::vector<Xfer> alltoall_xfers(int Nt, int Ny, int Nx, int W, bool forw
             split_planes(Nt, W, b, &tb, &nb);
             split_planes(Ny, W, a, &ya, &nya);
             split_planes(Ny, W, b, &yb, &nyb);
-            int64_t so, ro, n;
             if (forward) {
-                so = (int64_t)na * Nx * yb; n = (int64_t)na * nyb * Nx; ro = (int64_t)ta * nyb * Nx;
+                for (int tl = 0; tl < na; ++tl)
+                    if (nyb > 0)
+                        xs.push_back({a, b, tl * nxy + (int64_t)yb * Nx, (int64_t)(ta + tl) * nyb * Nx,
+                                      (int64_t)nyb * Nx});
             } else {
-                so = (int64_t)tb * nya * Nx; n = (int64_t)nb * nya * Nx; ro = (int64_t)nb * Nx * ya;
+                for (int tl = 0; tl < nb; ++tl)
+                    if (nya > 0)
+                        xs.push_back({a, b, (int64_t)(tb + tl) * nya * Nx, tl * nxy + (int64_t)ya * Nx,
+                                      (int64_t)nya * Nx});
             }
-            if (n > 0) xs.push_back({a, b, so, ro, n});
         }
     return xs;
 }

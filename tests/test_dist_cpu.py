@@ -12,7 +12,7 @@ tests/test_gpu_parity.py::test_bb_virtual_ranks_match_single.
 
 The default sharded CG (the spectral s-step CG, csrc/foto_bb.cpp cg_solve_spectral_sharded)
 is restated too: x/y DCTs of the own time planes, the slab -> row-box all-to-all with the
-library's packing and region arithmetic (k_spec_pack, alltoall_spec), the t-DCT on the box,
+library's region arithmetic (alltoall_xfers, one transfer per plane), the t-DCT on the box,
 s-step passes whose 48 Chebyshev moments are all-gathered and summed in rank order so that
 every rank plans identically (the numpy planning rule of tests/test_sstep_plan.py), and the
 way back.  It must reproduce scipy's CG (the oracle) on the same right-hand side.
@@ -325,53 +325,42 @@ def _exchange(sends, recvs):
 
 
 def _regions(Nt, Ny, Nx, W, a, b, forward):
-    """foto_bb.cpp alltoall_spec: what rank a sends to rank b (offsets and count, doubles)."""
+    """csrc/foto_xfer.h alltoall_xfers: what rank a sends to rank b, one (src offset, dst offset,
+    count) per plane, in doubles, between the natural slab layout and the row box."""
     ta, na = split_planes(Nt, W, a)
     tb, nb = split_planes(Nt, W, b)
     ya, nya = split_planes(Ny, W, a)
     yb, nyb = split_planes(Ny, W, b)
+    nxy = Nx * Ny
     if forward:
-        return na * Nx * yb, ta * nyb * Nx, na * nyb * Nx
-    return tb * nya * Nx, nb * Nx * ya, nb * nya * Nx
+        return [(tl * nxy + yb * Nx, (ta + tl) * nyb * Nx, nyb * Nx) for tl in range(na) if nyb]
+    return [((tb + tl) * nya * Nx, tl * nxy + ya * Nx, nya * Nx) for tl in range(nb) if nya]
 
 
 def _alltoall(S, sbuf, rsize, forward):
+    """the grouped sends / receives of alltoall_spec (one message per plane; a peer's messages in
+    list order, concatenated here as RCCL would deliver them one by one)"""
     W, g = S.W, S.rank
     rbuf = np.zeros(rsize)
     sends, recvs = [], []
     for h in range(W):
-        so, ro, n = _regions(S.Nt, S.Ny, S.Nx, W, g, h, forward)
+        regs = _regions(S.Nt, S.Ny, S.Nx, W, g, h, forward)
         if h == g:
-            if n:
+            for so, ro, n in regs:
                 rbuf[ro:ro + n] = sbuf[so:so + n]
             continue
-        if n:
-            sends.append((h, sbuf[so:so + n]))
-        so2, ro2, n2 = _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward)
-        if n2:
-            recvs.append((h, n2))
+        if regs:
+            sends.append((h, np.concatenate([sbuf[so:so + n] for so, _, n in regs])))
+        regs2 = _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward)
+        if regs2:
+            recvs.append((h, sum(n for _, _, n in regs2)))
     got = _exchange(sends, recvs)
     for h, buf in got.items():
-        _, ro2, n2 = _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward)
-        rbuf[ro2:ro2 + n2] = buf
+        at = 0
+        for _, ro, n in _regions(S.Nt, S.Ny, S.Nx, W, h, g, forward):
+            rbuf[ro:ro + n] = buf[at:at + n]
+            at += n
     return rbuf
-
-
-def _pack(S, planes, unpack_from=None):
-    """k_spec_pack: own planes [tl][y][x] <-> staging [h][tl][y - y0_h][x]."""
-    Ny, Nx, W, nloc = S.Ny, S.Nx, S.W, S.nloc
-    stage = np.zeros(nloc * Ny * Nx) if unpack_from is None else unpack_from
-    out = np.zeros((nloc, Ny, Nx))
-    for y in range(Ny):
-        h = _owner(Ny, W, y)
-        y0h, nyh = split_planes(Ny, W, h)
-        for tl in range(nloc):
-            j = nloc * Nx * y0h + (tl * nyh + (y - y0h)) * Nx
-            if unpack_from is None:
-                stage[j:j + Nx] = planes[tl, y]
-            else:
-                out[tl, y] = stage[j:j + Nx]
-    return stage if unpack_from is None else out
 
 
 def sharded_spectral_cg(S, F, r, eps, rtol=1e-6, maxiter=1000):
@@ -383,7 +372,7 @@ def sharded_spectral_cg(S, F, r, eps, rtol=1e-6, maxiter=1000):
     y0, nyl = split_planes(Ny, W, S.rank)
     # x, y DCTs of the own planes, slab -> box, t-DCT
     Fh = sfft.dct(sfft.dct(F, type=2, norm="ortho", axis=2), type=2, norm="ortho", axis=1)
-    box = _alltoall(S, _pack(S, Fh), Nt * nyl * Nx, True).reshape(Nt, nyl, Nx)
+    box = _alltoall(S, Fh.ravel(), Nt * nyl * Nx, True).reshape(Nt, nyl, Nx)
     bh = sfft.dct(box, type=2, norm="ortho", axis=0).ravel()
     mu = lambda n: 2 - 2 * np.cos(np.pi * np.arange(n) / n)  # noqa: E731
     lam = (r * eps + r * (mu(Nt)[:, None, None] + mu(Ny)[None, y0:y0 + nyl, None]
@@ -429,8 +418,7 @@ def sharded_spectral_cg(S, F, r, eps, rtol=1e-6, maxiter=1000):
         Mrr, Mrq, Mqq = moments(rr, q)
     # x^ = (b^ - r^) / lam, inverse t-DCT, box -> slab, inverse y, x
     xt = sfft.dct(((bh - rr) / lam).reshape(Nt, nyl, Nx), type=3, norm="ortho", axis=0)
-    stage = _alltoall(S, xt.ravel(), S.nloc * Ny * Nx, False)
-    phi = _pack(S, None, unpack_from=stage)
+    phi = _alltoall(S, xt.ravel(), S.nloc * Ny * Nx, False).reshape(S.nloc, Ny, Nx)
     phi = sfft.dct(sfft.dct(phi, type=3, norm="ortho", axis=1), type=3, norm="ortho", axis=2)
     return phi, k, log
 

@@ -32,7 +32,7 @@ def split(n, W, h):
 
 def calls(kind, Nt, Ny, Nx, W, rank, arg=0):
     from foto import _lib
-    cap = 4 * W * W + 8
+    cap = 4 * W * (Nt + W + 2) + 8   # (the all-to-all: one transfer per plane and peer)
     out = (ctypes.c_int64 * (5 * cap))()
     cnt = ctypes.c_int(0)
     _lib.check(_lib.lib().foto_xfer_calls(kind, Nt, Ny, Nx, W, rank, arg, out, cap, ctypes.byref(cnt)))
@@ -54,7 +54,7 @@ def src_extent(kind, Nt, Ny, Nx, W, g):
     if kind == XFER_HALO2:
         return 0, nl * nxy                      # own planes only (halos come from their owners)
     if kind == XFER_SLAB_TO_BOX:
-        return 0, nl * nxy                      # stage: [h][tl][rows of h][x]
+        return 0, nl * nxy                      # the slab [tl][y][x] (the rank's RHS buffer)
     if kind == XFER_BOX_TO_SLAB:
         return 0, Nt * nyl * Nx                 # box_out: [t][own rows][x]
     return 0, nxy                               # px / py / fu, fv, fm
@@ -71,7 +71,7 @@ def dst_extent(kind, Nt, Ny, Nx, W, g):
     if kind == XFER_SLAB_TO_BOX:
         return 0, max(Nt * nyl * Nx, nl * nxy)   # box_in (the spectral tmp buffer)
     if kind == XFER_BOX_TO_SLAB:
-        return 0, nl * nxy                       # stage
+        return 0, nl * nxy                       # the slab [tl][y][x]
     return 0, nxy
 
 
@@ -196,27 +196,20 @@ def test_replayed_exchanges_move_the_right_elements(shape, W):
     slabs = [split(Nt, W, g) for g in range(W)]
     boxes = [split(Ny, W, g) for g in range(W)]
 
-    # slab -> box: stage holds the rank's planes packed by destination rows (k_spec_pack)
-    stage = {}
-    for g, (t0, nl) in enumerate(slabs):
-        st = np.empty(nl * nxy)
-        for h, (y0, nyh) in enumerate(boxes):
-            st[nl * Nx * y0:nl * Nx * (y0 + nyh)] = G[t0:t0 + nl, y0:y0 + nyh, :].ravel()
-        stage[g] = (st, 0)
+    # slab -> box: straight from each rank's planes in their natural layout (one transfer per plane
+    # and destination box)
+    stage = {g: (G[t0:t0 + nl].ravel().copy(), 0) for g, (t0, nl) in enumerate(slabs)}
     box_in = {g: (np.full(max(Nt * boxes[g][1] * Nx, slabs[g][1] * nxy), np.nan), 0) for g in range(W)}
     replay(XFER_SLAB_TO_BOX, Nt, Ny, Nx, W, stage, box_in)
     for g, (y0, nyl) in enumerate(boxes):
         np.testing.assert_array_equal(box_in[g][0][:Nt * nyl * Nx].reshape(Nt, nyl, Nx), G[:, y0:y0 + nyl, :])
 
-    # box -> slab: the inverse (box_out = own rows of every plane) lands in stage layout
+    # box -> slab: the inverse (box_out = own rows of every plane) lands in the natural layout
     box_out = {g: (G[:, y0:y0 + nyl, :].ravel().copy(), 0) for g, (y0, nyl) in enumerate(boxes)}
     stage2 = {g: (np.full(slabs[g][1] * nxy, np.nan), 0) for g in range(W)}
     replay(XFER_BOX_TO_SLAB, Nt, Ny, Nx, W, box_out, stage2)
     for g, (t0, nl) in enumerate(slabs):
-        st = stage2[g][0]
-        for h, (y0, nyh) in enumerate(boxes):
-            np.testing.assert_array_equal(st[nl * Nx * y0:nl * Nx * (y0 + nyh)].reshape(nl, nyh, Nx),
-                                          G[t0:t0 + nl, y0:y0 + nyh, :])
+        np.testing.assert_array_equal(stage2[g][0].reshape(nl, Ny, Nx), G[t0:t0 + nl])
 
     # halos: planes -1 and nloc of every rank's padded field hold the neighbours' planes
     fields = {}
