@@ -25,18 +25,18 @@ struct SpectralPlan {
     const int* done_flag() const;
     int finish(int* iters, int* info, int* redo, KTimer* kt, hipStream_t s);
     int pending() const;
-    bool oldest_needs_redo() const;   // after the stream has passed the oldest solve's header copy
+    bool oldest_needs_redo() const;   // after the stream has passed the oldest solve's header store
     int drop_newest(hipStream_t s);
 
     // ---- sharded phases (driven by foto_bb.cpp, all-to-all / all-gather in between)
-    int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, pack -> stage
+    int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, in place in b (the all-to-all's source)
     int fwd_t(KTimer* kt, hipStream_t s);                   // box_in (after all-to-all) -> b^
     int cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s);   // r^ = b^, moments -> gath
     int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // planned CG steps, moments -> gath
     int cg_plan(int init, double rtol, int maxiter, hipStream_t s);      // after the all-gather
     int poll(int* done, int* iters, int* passes, hipStream_t s);
     int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
-    int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // unpack stage, inverse y, x
+    int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // inverse y, x of scratch (the all-to-all's target) -> x
     double* box_in() const;    // box-side receive buffer [t][rows][x]
     double* box_out() const;   // box-side send buffer of the inverse
     double* gath() const;      // world * moments() doubles
