@@ -43,7 +43,7 @@ METRIC = "BB solver iters/sec on 640×480×32 grid"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cg-mode", type=int, default=int(os.environ.get("FOTO_CG_MODE", "3")),
                     help="0 stencil CG, 1 spectral CG (one GPU), 2 spectral s-step CG, 3 Gauss-compressed spectral CG (default)")
