@@ -734,6 +734,13 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #ifndef FOTO_PR_Y
 #define FOTO_PR_Y 8
 #endif
+// mu' is read again only by the next outer iteration's prox, ~1.5 GB of other traffic later:
+// stored non-temporal it does not displace the lines the next kernels read (F, phi) --
+// 1646 -> 1655 it/s, the prox launch itself +1 us (A/B, profiles/r04n_ab_prox_nt.txt);
+// 2: F non-temporal too (the x-DCT reads it next: no better); 0: plain stores
+#ifndef FOTO_PR_NT
+#define FOTO_PR_NT 1
+#endif
 #ifndef FOTO_PR_X
 #define FOTO_PR_X 64
 #endif
@@ -856,9 +863,15 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
             stepb(p, opx, opy, ox, oy, mo, w, n0, a, gt, gx, gy, nu);
             if (mine) {
                 const int64_t i = p * nxy + ooff;
+#if FOTO_PR_NT
+                __builtin_nontemporal_store(nu[0], &nut[i]);
+                __builtin_nontemporal_store(nu[1], &nux[i]);
+                __builtin_nontemporal_store(nu[2], &nuy[i]);
+#else
                 nut[i] = nu[0];
                 nux[i] = nu[1];
                 nuy[i] = nu[2];
+#endif
                 const double gg = gx * gx + gy * gy;
                 num += n0 * fabs(gt + 0.5 * gg);
                 den += n0 * gg;
@@ -928,7 +941,11 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
             acc_d1w(s, oy, Ny, oy > 0 ? WY[ci - PR_PW] : 0.0, WY[ci], oy < Ny - 1 ? WY[ci + PR_PW] : 0.0);
             if (tn == 0) s -= (rho0[ooff] - bcm) + r * bcq;
             if (tn == Nt - 1) s += (rhoT[ooff] - bcm) + r * bcq;
+#if FOTO_PR_NT >= 2
+            __builtin_nontemporal_store(s, &F[n * nxy + ooff]);
+#else
             F[n * nxy + ooff] = s;
+#endif
             ff += s * s;
         }
         wtm = wtc;
