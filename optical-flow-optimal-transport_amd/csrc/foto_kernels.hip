@@ -741,6 +741,16 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #ifndef FOTO_PR_NT
 #define FOTO_PR_NT 1
 #endif
+// The old mu is dead after this kernel: the own voxels' loads are non-temporal (the ring
+// voxels' are re-read by the neighbouring tiles and stay plain) -- 1675-1688 -> 1708-1719
+// it/s, the DCT chain after it 130 -> 124 us (F stays cached for the x-DCT; A/B,
+// profiles/r04n_ab_nt_loads.txt).  0: plain loads.
+#ifndef FOTO_PR_NTLD
+#define FOTO_PR_NTLD 1
+#endif
+#ifndef FOTO_PR_NTPHI
+#define FOTO_PR_NTPHI 0  // 1: phi loaded non-temporal, 2: the ring voxels' mu too (A/B builds)
+#endif
 #ifndef FOTO_PR_X
 #define FOTO_PR_X 64
 #endif
@@ -808,7 +818,11 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         const bool ok = t0 + p >= 0 && p <= pz + 1 && t0 + p < Nt;
 #pragma unroll
         for (int j = 0; j < PR_FR; ++j)
+#if FOTO_PR_NTPHI == 1
+            v[j] = (ok && fin[j]) ? __builtin_nontemporal_load(&phi[p * nxy + foff[j]]) : 0.0;
+#else
             v[j] = (ok && fin[j]) ? phi[p * nxy + foff[j]] : 0.0;
+#endif
     };
     auto store_phi_from = [&](int p, const double (&v)[PR_FR]) {
 #pragma unroll
@@ -821,8 +835,24 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     double om[3] = {0.0, 0.0, 0.0}, hm[3] = {0.0, 0.0, 0.0};
     auto load_mu = [&](int p) {
         if (p > pz) return;
+#if FOTO_PR_NTLD
+        if (own) {   // (the old mu is dead after this kernel; ring voxels keep plain loads)
+            om[0] = __builtin_nontemporal_load(&mut[p * nxy + ooff]);
+            om[1] = __builtin_nontemporal_load(&mux[p * nxy + ooff]);
+            om[2] = __builtin_nontemporal_load(&muy[p * nxy + ooff]);
+        }
+#else
         if (own) { om[0] = mut[p * nxy + ooff]; om[1] = mux[p * nxy + ooff]; om[2] = muy[p * nxy + ooff]; }
+#endif
+#if FOTO_PR_NTPHI == 2
+        if (hal) {
+            hm[0] = __builtin_nontemporal_load(&mut[p * nxy + hoff]);
+            hm[1] = __builtin_nontemporal_load(&mux[p * nxy + hoff]);
+            hm[2] = __builtin_nontemporal_load(&muy[p * nxy + hoff]);
+        }
+#else
         if (hal) { hm[0] = mut[p * nxy + hoff]; hm[1] = mux[p * nxy + hoff]; hm[2] = muy[p * nxy + hoff]; }
+#endif
     };
     // stepB / stepC at stepB-region position (px, py) of local plane p (k_prox's body)
     auto stepb = [&](int p, int px, int py, int xg, int yg, const double (&m)[3], double (&w)[3], double& n0o,

@@ -627,6 +627,22 @@ static hipError_t dct_axis(int outer, int n, int inner, const double* M, const d
 #ifndef FOTO_FFT_LPB_POW2
 #define FOTO_FFT_LPB_POW2 1    // power-of-two line counts only (whole 128-B segments on strided axes)
 #endif
+// Loads of a pass's input that is dead after the pass (the DCT chain's intermediates, x^, b^
+// in the x^ kernel) are non-temporal: the lines leave the caches first, so the pass's output
+// and the next kernel's inputs keep them -- 1652-1660 -> 1667-1671 it/s, k_prox_rhs (after
+// the inverse x-DCT) 170-172 -> 167 us (A/B, profiles/r04n_ab_nt_loads.txt).  0: plain loads.
+#ifndef FOTO_NT_LD
+#define FOTO_NT_LD 1
+#endif
+template <class V>
+__device__ __forceinline__ V ld_dead(const V* p) {
+#if FOTO_NT_LD
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // Strided (y-axis) lines get a slightly larger LDS budget: at N = 1024 a line image is 8448 B,
 // so 64 KB held 4 lines (32-B row segments) and 68 KB holds 8 (64 B; still two blocks per CU)
 #ifndef FOTO_FFT_STRIDED_LDS
@@ -1013,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
             int l, j;
             if (CONTIG) { l = idx / N; j = idx - l * N; }
             else { j = idx / LPB; l = idx - j * LPB; }
-            xv[j0] = (RD::ok(idx) && l < f.nl) ? in[base(l) + j * st] : 0.0;
+            xv[j0] = (RD::ok(idx) && l < f.nl) ? ld_dead(&in[base(l) + j * st]) : 0.0;
         }
 #pragma unroll
         for (int j0 = 0; j0 < RD::R; ++j0) {
@@ -1100,10 +1116,10 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
         xk[j0] = xnk[j0] = xmk[j0] = xpk[j0] = 0.0;
         if (RP::ok(idx) && l < f.nl) {
             const double* X = in + base(l);
-            xk[j0] = X[k * st];
-            if (k != 0) xnk[j0] = X[(N - k) * st];
-            xmk[j0] = X[(M - k) * st];
-            if (M - k != 0) xpk[j0] = X[(N - (M - k)) * st];
+            xk[j0] = ld_dead(&X[k * st]);
+            if (k != 0) xnk[j0] = ld_dead(&X[(N - k) * st]);
+            xmk[j0] = ld_dead(&X[(M - k) * st]);
+            if (M - k != 0) xpk[j0] = ld_dead(&X[(N - (M - k)) * st]);
         }
     }
 #pragma unroll
@@ -2468,7 +2484,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
         if (c >= ncols) return;
         double x[NTT];
 #pragma unroll
-        for (int j = 0; j < NTT; ++j) x[j] = in[j * ncols + c];
+        for (int j = 0; j < NTT; ++j) x[j] = ld_dead(&in[j * ncols + c]);
 #pragma unroll
         for (int m = 0; m < H; ++m) {
             double e = 0.0, o = 0.0;
@@ -2564,7 +2580,7 @@ __global__ __launch_bounds__(TC_NTH) __attribute__((amdgpu_waves_per_eu(FOTO_TC_
             const int k = 2 * m + p;
             double v;
             if constexpr (PLAIN) {
-                v = bh[k * ncols + c];
+                v = ld_dead(&bh[k * ncols + c]);
             } else {
                 const double lam = spec_lam(T, T.mt[k] + T.my[ky], kx);
                 v = (bh[k * ncols + c] - rh[k * ncols + c]) / lam;
