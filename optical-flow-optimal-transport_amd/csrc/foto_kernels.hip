@@ -741,15 +741,15 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #ifndef FOTO_PR_NT
 #define FOTO_PR_NT 1
 #endif
-// The old mu is dead after this kernel: the own voxels' loads are non-temporal (the ring
-// voxels' are re-read by the neighbouring tiles and stay plain) -- 1675-1688 -> 1708-1719
-// it/s, the DCT chain after it 130 -> 124 us (F stays cached for the x-DCT; A/B,
-// profiles/r04n_ab_nt_loads.txt).  0: plain loads.
+// The old mu is dead after this kernel: its loads are non-temporal.  Own voxels only (1):
+// 1675-1688 -> 1708-1719 it/s, the DCT chain after it 130 -> 124 us (F stays cached for the
+// x-DCT); the ring voxels' loads too (2, default): 1690-1716 -> 1703-1740, the prox launch
+// unchanged (A/B, profiles/r04n_ab_nt_loads.txt).  0: plain loads.
 #ifndef FOTO_PR_NTLD
-#define FOTO_PR_NTLD 1
+#define FOTO_PR_NTLD 2
 #endif
 #ifndef FOTO_PR_NTPHI
-#define FOTO_PR_NTPHI 0  // 1: phi loaded non-temporal, 2: the ring voxels' mu too (A/B builds)
+#define FOTO_PR_NTPHI 0  // 1: phi loaded non-temporal (prox 165 -> 173 us: its halo is re-read)
 #endif
 #ifndef FOTO_PR_X
 #define FOTO_PR_X 64
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
 #else
         if (own) { om[0] = mut[p * nxy + ooff]; om[1] = mux[p * nxy + ooff]; om[2] = muy[p * nxy + ooff]; }
 #endif
-#if FOTO_PR_NTPHI == 2
+#if FOTO_PR_NTLD >= 2
         if (hal) {
             hm[0] = __builtin_nontemporal_load(&mut[p * nxy + hoff]);
             hm[1] = __builtin_nontemporal_load(&mux[p * nxy + hoff]);
