@@ -141,9 +141,15 @@ class FileRendezvous:
         return max(float(open(p).read()) for p in names)
 
     def close(self):
-        self.barrier()
+        """Every rank but 0 leaves its final file and returns at once; rank 0 waits for all of
+        them before it removes the directory, so no rank can still be polling for a file of a
+        removed directory (a full barrier here let rank 0 delete the files a slower rank was
+        about to check, and that rank then timed out)."""
+        self.n += 1
+        self._put(f"end{self.n}_{self.rank}", b"")
         if self.rank == 0:
             import shutil
+            self._wait([os.path.join(self.dir, f"end{self.n}_{g}") for g in range(self.world)])
             shutil.rmtree(self.dir, ignore_errors=True)
 
 

@@ -102,7 +102,7 @@ typedef struct {
     /* per kernel class (timing = 1): launches and summed device time in ms            */
     int64_t n_k[8];
     double ms_k[8];
-    double bytes_k[8];        /* algorithmic HBM bytes per launch of that class         */
+    double bytes_k[8];        /* algorithmic HBM bytes of those launches, summed        */
     int cg_redo;              /* outer iterations whose deferred CG solve (see foto_bb.cpp) */
                               /* outran its predicted passes and re-ran prox             */
 } foto_bb_stats;
@@ -123,7 +123,13 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
 /* Run up to `max_iters` outer iterations (stepA + stepB + stepC + criterion).  With
  * use_stop_rules = 1 it stops like the reference (crit <= tol, or |dcrit| < 1e-5).
  * cb (may be NULL) gets (iteration index, crit, CG iterations, CG info) after each
- * outer iteration.  Returns 1 if a stop rule fired, 0 otherwise, < 0 on error.    */
+ * outer iteration.  Returns 1 if a stop rule fired, 0 otherwise, < 0 on error.
+ * The callback runs while the NEXT outer iteration is already on the stream.  In the
+ * default single-GPU loop (two iterations in flight) foto_bb_get_phi / get_state / flow
+ * called from it return the state of the iteration the callback reports (kept intact for a
+ * rollback); the one-in-flight loop (sharded, FOTO_PIPE=0) refuses them there with
+ * FOTO_ERR_STATE (its next solve overwrites phi).  An error with iterations in flight drains
+ * the stream and leaves the context refusing iterate / flow until foto_bb_reset.        */
 int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double convergence_tol, int use_stop_rules,
                     foto_bb_iter_cb cb, void* user, int* iters_done);
 /* Flow (u, v, m) from the last phi: utils.opticalflow_from_benamoubrenier.
@@ -132,7 +138,8 @@ int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m);
 /* A new pair (rho0, rhoT) of the same size on an existing context: every field, counter and
  * prediction back to what foto_bb_create leaves, so the solve is bit-identical to one on a
  * fresh context -- without its allocations, DCT plans and stream (a batch of same-size
- * frames: run.sh:81-157 runs one solve per sequence).                                     */
+ * frames: run.sh:81-157 runs one solve per sequence).  Also the way back after a failed
+ * foto_bb_iterate (whatever it left on the stream is drained first).                     */
 int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT);
 /* Copy this shard's slab range of phi / mu / q to host (t0, nloc via foto_bb_shard). */
 int foto_bb_get_phi(foto_bb_ctx* c, double* phi);
@@ -150,6 +157,36 @@ void foto_bb_destroy(foto_bb_ctx* c);
 int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r,
                   double convergence_tol, double reg_epsilon, int max_it, foto_bb_iter_cb cb, void* user,
                   double* u, double* v, double* m);
+
+/* Per-solve report of foto_bb_solve_ex (outer iterations, the per-iteration
+ * crit and CG counts, per-phase time and HBM bytes).  The caller owns the three arrays (any may
+ * be NULL) and sets cap to their length; entries beyond cap are counted but not stored.       */
+typedef struct {
+    int cap;                  /* in: length of crit / cg_its / cg_info                        */
+    double* crit;             /* out: crit of outer iteration i (benamou_brenier.py:249)       */
+    int* cg_its;              /* out: CG iterations of that stepA (scipy cg at :85)           */
+    int* cg_info;             /* out: CG info (0 converged, maxiter otherwise; :86-87 warning) */
+    int outer_iters;          /* out: outer iterations run                                    */
+    int stopped;              /* out: 1 if a stop rule ended the run (:253-258)               */
+    int phi_t0, phi_nloc;     /* out: the time planes phi_or_null received (this rank's slab) */
+    double ms_create;         /* out: host wall time of context creation (uploads, plans)     */
+    double ms_loop;           /* out: host wall time of the outer-iteration loop (the metric) */
+    double ms_flow;           /* out: host wall time of the flow extraction + download        */
+    double alg_bytes_per_iter;/* out: algorithmic HBM bytes of one outer iteration on this
+                                 rank (188 B per voxel for the default path)     */
+    foto_bb_stats bb;         /* out: the context's counters (kernel classes with opts.timing) */
+} foto_bb_solve_stats;
+
+/* One-shot benamou_brenier.solve (benamou_brenier.py:151-271) with the options of a context
+ * (opts may be NULL: foto_bb_opts_default; opts->world > 1: this process is rank opts->rank of
+ * a time-slab sharded solve over RCCL -- config 4 -- and every rank calls it with the same
+ * arguments), the reference's stop rules, and the per-solve report above.  (u, v, m) land on
+ * rank 0 (other ranks may pass NULL); phi_or_null gets this rank's slab of the last phi
+ * (st->phi_t0, st->phi_nloc planes; all Nt planes on one GPU).  st may be NULL.  Returns 0,
+ * or < 0 on error; CG non-convergence is reported in st->cg_info (a warning, not an error). */
+int foto_bb_solve_ex(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r,
+                     double convergence_tol, double reg_epsilon, int max_it, const foto_bb_opts* opts,
+                     double* u, double* v, double* m, double* phi_or_null, foto_bb_solve_stats* st);
 
 /* RCCL unique id for foto_bb_opts.nccl_id (call on rank 0, broadcast 128 bytes). */
 int foto_nccl_unique_id(void* out128);
@@ -205,6 +242,22 @@ int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3);
  * libraries cache plans; FOTO_GN_PLAN_CACHE=0 makes and destroys one per call.       */
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
                   double rtol, int maxiter, double* u, double* v, double* m, int* iterations);
+
+/* Per-solve report of foto_gn_solve_ex (SURVEY.md §8(b) foto_gn_stats).                      */
+typedef struct {
+    int iterations;           /* PCG iterations run                                            */
+    int info;                 /* 0 converged, maxiter otherwise (the return value)             */
+    int plan_reused;          /* 1: the cached plan of the previous call served this one       */
+    int levels;               /* multigrid levels of the preconditioner                        */
+    double ms_setup;          /* device time: upload, coefficients, RHS, V-cycle of r0          */
+    double ms_pcg;            /* device time of the PCG iterations                             */
+    double ms_total;          /* host wall time of the call                                    */
+    double alg_bytes_per_iter;/* algorithmic HBM bytes of one PCG iteration   */
+} foto_gn_stats;
+
+/* foto_gn_solve with the report above (st may be NULL).                                      */
+int foto_gn_solve_ex(const double* f1, const double* f2, int w, int h, double alpha, double lambda_,
+                     double rtol, int maxiter, double* u, double* v, double* m, foto_gn_stats* st);
 
 /* A reusable GLLOpticalFlow(w, h) with setAlpha/setLambda applied (classical.py:25-66): device
  * buffers, the multigrid hierarchy and the replayed PCG graph are made once; every

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstddef>
@@ -192,6 +193,9 @@ struct foto_bb_ctx {
         bool pev;                      // phase events recorded (ph[par][0..3])
     };
     std::vector<Enq> inflight;   // oldest first
+    // an iterate call failed with iterations on the stream: they were drained (drain_inflight),
+    // the host state no longer matches the device's, so only foto_bb_reset brings it back
+    bool broken = false;
     // bookkeeping
     double prev_crit = -1;
     foto_bb_stats st{};
@@ -770,6 +774,48 @@ static int rollback(foto_bb_ctx* c) {
     return 0;
 }
 
+// After an error with outer iterations on the stream: wait for the stream (errors ignored: the
+// one being reported is the first), forget their deferred solves and timings, and leave no
+// record behind, so foto_bb_reset can start over.
+static void drain_inflight(foto_bb_ctx* c) {
+    if (c->inflight.empty()) return;
+    (void)hipStreamSynchronize(c->s);
+    for (auto it = c->inflight.rbegin(); it != c->inflight.rend(); ++it)
+        if (it->dsp) (void)it->dsp->drop_newest(c->s);
+    c->kt.discard_from(c->inflight.front().kmark);
+    c->inflight.clear();
+    c->broken = true;
+}
+
+// The host pointers of the last COMPLETED outer iteration.  Inside the iteration callback the
+// next iteration is already on the stream and the shard's pointers are its own; the pipelined
+// loop keeps the completed iteration's phi and mu intact (the record of the one in flight holds
+// them), the one-in-flight loop does not (its next solve overwrites phi), so there a call from
+// the callback is refused.
+struct Completed {
+    double* phi;
+    double* mu[3];
+    double* fz_src[3];
+};
+static int completed_state(foto_bb_ctx* c, const char* who, Completed* out) {
+    Shard& s0 = *c->sh[0];
+    if (c->inflight.empty()) {
+        out->phi = s0.phi;
+        for (int f = 0; f < 3; ++f) { out->mu[f] = s0.mu[f]; out->fz_src[f] = s0.fz_src[f]; }
+        return 0;
+    }
+    if (!c->pipe) {
+        set_error("%s: called while the next outer iteration is on the stream (from the iteration callback of "
+                  "the one-in-flight loop, whose next solve overwrites phi); call it after foto_bb_iterate returns",
+                  who);
+        return FOTO_ERR_STATE;
+    }
+    const foto_bb_ctx::Enq& e = c->inflight.front();
+    out->phi = e.phi;
+    for (int f = 0; f < 3; ++f) { out->mu[f] = e.mu[f]; out->fz_src[f] = e.fz_src[f]; }
+    return 0;
+}
+
 static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_info) {
     const int W = c->W;
     if (c->inflight.empty()) {
@@ -1016,10 +1062,27 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
     return 0;
 }
 
+static int iterate_loop(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rules, foto_bb_iter_cb cb,
+                        void* user, int* iters_done);
+
 int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rules, foto_bb_iter_cb cb, void* user,
                     int* iters_done) {
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
+    if (iters_done) *iters_done = 0;
+    if (c->broken) {
+        set_error("foto_bb_iterate: a previous call failed with outer iterations in flight; foto_bb_reset the context");
+        return FOTO_ERR_STATE;
+    }
     if (!c->inflight.empty()) { set_error("foto_bb_iterate: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
+    const int rc = iterate_loop(c, max_iters, tol, use_stop_rules, cb, user, iters_done);
+    if (rc < 0) drain_inflight(c);   // (an error leaves no record behind; only a reset continues)
+    return rc;
+}
+
+}  // extern "C"
+
+static int iterate_loop(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rules, foto_bb_iter_cb cb,
+                        void* user, int* iters_done) {
     int done = 0;
     int stopped = 0;
     auto stop_test = [&](double crit) {
@@ -1090,9 +1153,12 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
     return stopped;
 }
 
+extern "C" {
+
 int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     if (!c || !rho0 || !rhoT) { set_error("null argument"); return FOTO_ERR_ARG; }
-    if (!c->inflight.empty()) { set_error("foto_bb_reset: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
+    drain_inflight(c);   // (normally empty: foto_bb_iterate drains on error)
+    c->broken = false;
     const int64_t nxy = (int64_t)c->Nx * c->Ny;
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
     for (auto& sp : c->sh) {
@@ -1131,7 +1197,16 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
 
 int foto_bb_flow(foto_bb_ctx* c, double* u, double* v, double* m) {
     if (!c) { set_error("null ctx"); return FOTO_ERR_ARG; }
-    return flow(c, u, v, m);
+    if (c->broken) { set_error("foto_bb_flow: a failed foto_bb_iterate left the context inconsistent; foto_bb_reset it"); return FOTO_ERR_STATE; }
+    Completed k;
+    FOTO_TRY(completed_state(c, "foto_bb_flow", &k));
+    // (pipelined loop, from the callback: the completed iteration's phi, then the one in flight's back)
+    Shard& s0 = *c->sh[0];
+    double* keep = s0.phi;
+    s0.phi = k.phi;
+    const int rc = flow(c, u, v, m);
+    s0.phi = keep;
+    return rc;
 }
 
 int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc) {
@@ -1143,10 +1218,13 @@ int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc) {
 
 int foto_bb_get_phi(foto_bb_ctx* c, double* phi) {
     if (!c || !phi) return FOTO_ERR_ARG;
+    Completed k;
+    FOTO_TRY(completed_state(c, "foto_bb_get_phi", &k));
     size_t off = 0;
     for (auto& sp : c->sh) {
         const size_t n = (size_t)sp->g.nloc * sp->g.nxy;
-        FOTO_HIP_CHECK(hipMemcpyAsync(phi + off, sp->phi, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        const double* src = (sp.get() == c->sh[0].get()) ? k.phi : sp->phi;
+        FOTO_HIP_CHECK(hipMemcpyAsync(phi + off, src, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
         off += n;
     }
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
@@ -1155,11 +1233,15 @@ int foto_bb_get_phi(foto_bb_ctx* c, double* phi) {
 
 int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3) {
     if (!c) return FOTO_ERR_ARG;
+    Completed k;
+    FOTO_TRY(completed_state(c, "foto_bb_get_state", &k));
+    auto is0 = [&](const Shard& s) { return &s == c->sh[0].get(); };
     if (q3 && c->fuse && c->have_phi) {   // the fused kernel never stores q: recompute it (bit-identical)
         for (auto& sp : c->sh) {   // (phi's halo planes are the ones the last prox read)
             Shard& s = *sp;
-            if (!s.fz_src[0]) continue;
-            FOTO_HIP_CHECK(launch_q_from_phi(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.q[0], s.q[1],
+            double* const* src = is0(s) ? k.fz_src : s.fz_src;
+            if (!src[0]) continue;
+            FOTO_HIP_CHECK(launch_q_from_phi(s.g, is0(s) ? k.phi : s.phi, src[0], src[1], src[2], s.q[0], s.q[1],
                                              s.q[2], c->r, c->s));
         }
     }
@@ -1169,7 +1251,8 @@ int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3) {
         size_t off = 0;
         for (auto& sp : c->sh) {
             const size_t n = (size_t)sp->g.nloc * sp->g.nxy;
-            if (mu3) FOTO_HIP_CHECK(hipMemcpyAsync(mu3 + f * tot + off, sp->mu[f], n * 8, hipMemcpyDeviceToHost, c->s));
+            const double* mu = is0(*sp) ? k.mu[f] : sp->mu[f];
+            if (mu3) FOTO_HIP_CHECK(hipMemcpyAsync(mu3 + f * tot + off, mu, n * 8, hipMemcpyDeviceToHost, c->s));
             if (q3) FOTO_HIP_CHECK(hipMemcpyAsync(q3 + f * tot + off, sp->q[f], n * 8, hipMemcpyDeviceToHost, c->s));
             off += n;
         }
@@ -1220,6 +1303,80 @@ int foto_bb_solve(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny
     return rc < 0 ? rc : 0;
 }
 
+namespace {
+struct SolveLog {
+    foto_bb_solve_stats* st;
+    int n = 0;
+    int64_t cg = 0;
+};
+void solve_log_cb(void* user, int, double crit, int its, int info) {
+    SolveLog* L = (SolveLog*)user;
+    foto_bb_solve_stats* st = L->st;
+    if (st && L->n < st->cap) {
+        if (st->crit) st->crit[L->n] = crit;
+        if (st->cg_its) st->cg_its[L->n] = its;
+        if (st->cg_info) st->cg_info[L->n] = info;
+    }
+    L->n += 1;
+    L->cg += its;
+}
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
+int foto_bb_solve_ex(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r, double tol, double eps,
+                     int max_it, const foto_bb_opts* opts, double* u, double* v, double* m, double* phi_or_null,
+                     foto_bb_solve_stats* st) {
+    if (max_it <= 0) {
+        set_error("max_it = %d: the reference's loop never runs and phi is unbound (benamou_brenier.py:271, "
+                  "UnboundLocalError)", max_it);
+        return FOTO_ERR_STATE;
+    }
+    if (st) {   // (the caller's arrays and cap stay; every output field starts at zero)
+        const foto_bb_solve_stats keep = *st;
+        memset(st, 0, sizeof(*st));
+        st->cap = std::max(0, keep.cap);
+        st->crit = keep.crit; st->cg_its = keep.cg_its; st->cg_info = keep.cg_info;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    foto_bb_ctx* c = nullptr;
+    FOTO_TRY(foto_bb_create(rho0, rhoT, Nt, Nx, Ny, r, eps, opts, &c));
+    std::unique_ptr<foto_bb_ctx> guard(c);
+    if (st) st->ms_create = ms_since(t0);
+    SolveLog L{st};
+    int done = 0;
+    t0 = std::chrono::steady_clock::now();
+    const int rc = foto_bb_iterate(c, max_it, tol, 1, solve_log_cb, &L, &done);
+    if (rc < 0) return rc;
+    FOTO_TRY(foto_bb_sync(c));
+    const double ms_loop = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
+    FOTO_TRY(foto_bb_flow(c, u, v, m));
+    if (phi_or_null) FOTO_TRY(foto_bb_get_phi(c, phi_or_null));
+    FOTO_TRY(foto_bb_sync(c));
+    if (st) {
+        st->ms_flow = ms_since(t0);
+        st->ms_loop = ms_loop;
+        st->outer_iters = L.n;
+        st->stopped = rc;
+        FOTO_TRY(foto_bb_shard(c, &st->phi_t0, &st->phi_nloc));
+        FOTO_TRY(foto_bb_stats_get(c, &st->bb));
+        // the algorithmic bytes of one outer iteration on this rank: the default path's itemised
+        // 188 B per voxel (bench.py STEP_BYTES_PER_VOXEL), the literal stencil
+        // CG's (21 + 10 k) 8 B; the other modes from the kernel timers
+        const double nv = (double)st->phi_nloc * (double)Nx * (double)Ny;
+        if (c->o.cg_mode == 3) st->alg_bytes_per_iter = 188.0 * nv;
+        else if (c->o.cg_mode == 0 && L.n > 0) st->alg_bytes_per_iter = (21.0 + 10.0 * (double)L.cg / L.n) * 8.0 * nv;
+        else if (L.n > 0) {
+            double b = 0;
+            for (int k = 0; k < 8; ++k) b += st->bb.bytes_k[k];   // (summed over the launches)
+            st->alg_bytes_per_iter = b / L.n;   // (0 without opts->timing)
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"
 
 extern "C" int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double eps, double rtol, int maxiter, int mode,
@@ -1250,3 +1407,8 @@ extern "C" int foto_cg(const double* b, int Nt, int Nx, int Ny, double r, double
 // ctypes mirrors these layouts (foto/_lib.py); tests/test_cabi.py checks the Python side.
 static_assert(sizeof(foto_bb_opts) == 48, "foto_bb_opts layout");
 static_assert(offsetof(foto_bb_stats, n_k) == 56, "foto_bb_stats layout");
+static_assert(sizeof(foto_bb_stats) == 256, "foto_bb_stats layout");
+static_assert(offsetof(foto_bb_solve_stats, ms_create) == 48 && offsetof(foto_bb_solve_stats, bb) == 80 &&
+                  sizeof(foto_bb_solve_stats) == 336,
+              "foto_bb_solve_stats layout");
+static_assert(sizeof(foto_gn_stats) == 48, "foto_gn_stats layout");

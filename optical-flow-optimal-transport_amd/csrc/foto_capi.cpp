@@ -3,6 +3,7 @@
 // the caller's host buffers to the current device, runs the kernels on a private stream
 // and copies the result back; device scratch lives only for the call.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -274,8 +275,47 @@ int foto_gn_rhs(const double* f1, const double* f2, int w, int h, double* b3) {
 
 // classical.GLLOpticalFlow.process: PCG to rtol on the assembled-equivalent operator.
 // Device-resident loop; the host polls the done flag between chunks of iterations.
+static int gn_solve_impl(const double* f1, const double* f2, int w, int h, double alpha, double lam, double rtol,
+                         int maxiter, double* u, double* v, double* m, int* iterations, foto_gn_stats* st);
+
 int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha, double lam, double rtol,
                   int maxiter, double* u, double* v, double* m, int* iterations) {
+    return gn_solve_impl(f1, f2, w, h, alpha, lam, rtol, maxiter, u, v, m, iterations, nullptr);
+}
+
+// Algorithmic HBM bytes of one MG-PCG iteration (bench.py gn_bytes_per_iteration):
+// k_gnp_dir 12 n, k_gnp_upd 18 n, per level k_mg_down2 18 n_l + 3 n_l+1 and k_mg_up2 21 n_l + 3 n_l+1,
+// the coarsest level 18 n_c fp64 values; levels halve (rounding up) until <= 1024 cells.
+static double gn_alg_bytes(int w, int h, int* levels) {
+    std::vector<double> ns{(double)w * h};
+    while ((double)w * h > 1024) {
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+        ns.push_back((double)w * h);
+    }
+    double v = 30.0 * ns[0];
+    for (size_t l = 0; l + 1 < ns.size(); ++l) v += 39.0 * ns[l] + 6.0 * ns[l + 1];
+    v += 18.0 * ns.back();
+    if (levels) *levels = (int)ns.size();
+    return 8.0 * v;
+}
+
+int foto_gn_solve_ex(const double* f1, const double* f2, int w, int h, double alpha, double lam, double rtol,
+                     int maxiter, double* u, double* v, double* m, foto_gn_stats* st) {
+    int its = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (st) memset(st, 0, sizeof(*st));
+    const int rc = gn_solve_impl(f1, f2, w, h, alpha, lam, rtol, maxiter, u, v, m, &its, st);
+    if (rc >= 0 && st) {
+        st->iterations = its;
+        st->info = rc;
+        st->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rc;
+}
+
+static int gn_solve_impl(const double* f1, const double* f2, int w, int h, double alpha, double lam, double rtol,
+                         int maxiter, double* u, double* v, double* m, int* iterations, foto_gn_stats* st) {
     FOTO_TRY(check2(w, h));
     if (!(alpha > 0) || !(lam > 0)) {
         set_error("GN needs alpha > 0 and lambda > 0 (the block-Jacobi preconditioner divides by them)");
@@ -297,13 +337,22 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
         std::lock_guard<std::mutex> lk(mu);
         int dev = 0;
         FOTO_HIP_CHECK(hipGetDevice(&dev));
-        if (!cache || !cached || memcmp(key, k6, sizeof(k6)) != 0 || foto_gn_plan_device(cached) != dev) {
+        const bool reused = !(!cache || !cached || memcmp(key, k6, sizeof(k6)) != 0 || foto_gn_plan_device(cached) != dev);
+        if (!reused) {
             foto_gn_plan_destroy(cached);
             cached = nullptr;
             FOTO_TRY(foto_gn_plan_create(w, h, alpha, lam, rtol, maxiter, &cached));
             memcpy(key, k6, sizeof(k6));
         }
         const int rc = foto_gn_plan_solve(cached, f1, f2, u, v, m, iterations);
+        if (st && rc >= 0) {
+            double t4[4];
+            FOTO_TRY(foto_gn_plan_timing(cached, t4));
+            st->ms_setup = t4[0];
+            st->ms_pcg = t4[1];
+            st->plan_reused = reused ? 1 : 0;
+            st->alg_bytes_per_iter = gn_alg_bytes(w, h, &st->levels);
+        }
         if (!cache || rc < 0) {
             foto_gn_plan_destroy(cached);
             cached = nullptr;
@@ -363,6 +412,10 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
     FOTO_TRY(S.down(m, x + 2 * n, n));
     FOTO_TRY(S.sync());
     if (iterations) *iterations = done ? hS->iters : maxiter;
+    if (st) {   // (no plan, no multigrid: 3 fields of 10 + 3 coefficient + 6 block-inverse values)
+        st->levels = 0;
+        st->alg_bytes_per_iter = 8.0 * (double)n * (3 * 10 + 3 + 6);
+    }
     return done ? 0 : maxiter;
 }
 

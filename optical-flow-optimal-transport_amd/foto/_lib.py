@@ -56,6 +56,39 @@ class BBStats(ctypes.Structure):
     ]
 
 
+class BBSolveStats(ctypes.Structure):
+    """foto_bb_solve_stats (include/foto.h): the caller sizes crit / cg_its / cg_info by cap."""
+    _fields_ = [
+        ("cap", ctypes.c_int),
+        ("crit", ctypes.POINTER(ctypes.c_double)),
+        ("cg_its", ctypes.POINTER(ctypes.c_int)),
+        ("cg_info", ctypes.POINTER(ctypes.c_int)),
+        ("outer_iters", ctypes.c_int),
+        ("stopped", ctypes.c_int),
+        ("phi_t0", ctypes.c_int),
+        ("phi_nloc", ctypes.c_int),
+        ("ms_create", ctypes.c_double),
+        ("ms_loop", ctypes.c_double),
+        ("ms_flow", ctypes.c_double),
+        ("alg_bytes_per_iter", ctypes.c_double),
+        ("bb", BBStats),
+    ]
+
+
+class GNStats(ctypes.Structure):
+    """foto_gn_stats (include/foto.h)."""
+    _fields_ = [
+        ("iterations", ctypes.c_int),
+        ("info", ctypes.c_int),
+        ("plan_reused", ctypes.c_int),
+        ("levels", ctypes.c_int),
+        ("ms_setup", ctypes.c_double),
+        ("ms_pcg", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+        ("alg_bytes_per_iter", ctypes.c_double),
+    ]
+
+
 ITER_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int)
 
 _D = ctypes.POINTER(ctypes.c_double)
@@ -93,6 +126,8 @@ SIGNATURES = {
     "foto_bb_sync": (_I, [_P]),
     "foto_bb_destroy": (None, [_P]),
     "foto_bb_solve": (_I, [_D, _D, _I, _I, _I, _Dbl, _Dbl, _Dbl, _I, ITER_CB, _P, _D, _D, _D]),
+    "foto_bb_solve_ex": (_I, [_D, _D, _I, _I, _I, _Dbl, _Dbl, _Dbl, _I, ctypes.POINTER(BBOpts), _D, _D, _D, _D,
+                              ctypes.POINTER(BBSolveStats)]),
     "foto_nccl_unique_id": (_I, [_P]),
     "foto_xfer_calls": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_int64), _I, ctypes.POINTER(_I)]),
     "foto_dct": (_I, [_D, _I, _I, _I, _I, _I, _D]),
@@ -101,6 +136,7 @@ SIGNATURES = {
     "foto_gn_apply": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _D, _D]),
     "foto_gn_rhs": (_I, [_D, _D, _I, _I, _D]),
     "foto_gn_solve": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _Dbl, _I, _D, _D, _D, ctypes.POINTER(_I)]),
+    "foto_gn_solve_ex": (_I, [_D, _D, _I, _I, _Dbl, _Dbl, _Dbl, _I, _D, _D, _D, ctypes.POINTER(GNStats)]),
     "foto_gn_plan_create": (_I, [_I, _I, _Dbl, _Dbl, _Dbl, _I, ctypes.POINTER(_P)]),
     "foto_gn_plan_solve": (_I, [_P, _D, _D, _D, _D, _D, ctypes.POINTER(_I)]),
     "foto_gn_plan_timing": (_I, [_P, _D]),

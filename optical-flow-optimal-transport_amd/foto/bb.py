@@ -108,7 +108,10 @@ class BBSolver:
     # -------------------------------------------------------------- iterations
     def iterate(self, n, convergence_tol=0.0, stop_rules=True, callback=None):
         """Run up to n outer iterations; returns True if a reference stop rule fired.
-        ``callback(i, crit, cg_its, cg_info)`` is called after each iteration."""
+        ``callback(i, crit, cg_its, cg_info)`` is called after each iteration, while iteration
+        i + 1 is already on the stream: in the default single-GPU loop ``phi()``, ``state()``
+        and ``flow()`` called from it return iteration i's results; the one-in-flight loop
+        (sharded contexts, FOTO_PIPE=0) raises FotoError for them there (foto.h)."""
         errors = []
 
         def _cb(user, it, crit, its, info):
@@ -243,6 +246,57 @@ def solve(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, ma
             raise
     with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=reg_epsilon, **opts) as s:
         return _run(s, max_it, convergence_tol, cb, stats)
+
+
+def solve_ex(rho0, rhoT, Nt, Nx, Ny, r=1, convergence_tol=0.3, reg_epsilon=1e-3, max_it=100, *, cap=None,
+             want_phi=True, device=-1, cg_mode=CG_GAUSS, cg_rtol=1e-6, cg_maxiter=1000, rank=0, world=1,
+             nccl_id=None, virtual_ranks=1, timing=False, library=None):
+    """benamou_brenier.solve through the one-shot C entry foto_bb_solve_ex (include/foto.h; the
+    SURVEY.md §8(b) boundary): a context made, iterated with the reference's stop rules, the flow
+    extracted and the context destroyed in one call.  Returns (u, v, m, report): report holds the
+    per-outer-iteration crit / cg_its / cg_info (the first ``cap`` of them, default max_it), phi
+    (this rank's slab) and the timings and byte counts of foto_bb_solve_stats.  With world > 1
+    every rank calls it; (u, v, m) are None off rank 0."""
+    L = library if library is not None else lib()
+    Nt, Nx, Ny = int(Nt), int(Nx), int(Ny)
+    nxy = Nx * Ny
+    a0, aT = f64(rho0, nxy, "rho0"), f64(rhoT, nxy, "rhoT")
+    o = _lib.BBOpts()
+    L.foto_bb_opts_default(ctypes.byref(o))
+    o.device, o.cg_mode, o.cg_rtol, o.cg_maxiter = int(device), int(cg_mode), float(cg_rtol), int(cg_maxiter)
+    o.rank, o.world, o.virtual_ranks, o.timing = int(rank), int(world), int(virtual_ranks), 1 if timing else 0
+    idbuf = None
+    if nccl_id is not None:
+        idbuf = ctypes.create_string_buffer(bytes(nccl_id), 128)
+        o.nccl_id = ctypes.cast(idbuf, ctypes.c_void_p)
+    cap = int(max_it if cap is None else cap)
+    crit = np.zeros(max(cap, 1))
+    its = np.zeros(max(cap, 1), dtype=np.int32)
+    info = np.zeros(max(cap, 1), dtype=np.int32)
+    st = _lib.BBSolveStats()
+    st.cap = cap
+    st.crit = dptr(crit)
+    st.cg_its = its.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    st.cg_info = info.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    on0 = int(world) == 1 or int(rank) == 0
+    u, v, m = (np.empty(nxy) for _ in range(3)) if on0 else (None, None, None)
+    # the largest slab a rank can hold (split_planes: balanced), or every plane on one GPU
+    phi = np.empty(-(-Nt // max(int(world), 1)) * nxy) if want_phi else None
+    null = _lib._D()
+    check(L.foto_bb_solve_ex(dptr(a0), dptr(aT), Nt, Nx, Ny, float(r), float(convergence_tol), float(reg_epsilon),
+                             int(max_it), ctypes.byref(o), dptr(u) if on0 else null, dptr(v) if on0 else null,
+                             dptr(m) if on0 else null, dptr(phi) if want_phi else null, ctypes.byref(st)), L)
+    n = min(st.outer_iters, cap)
+    rep = {"outer_iters": st.outer_iters, "stopped": bool(st.stopped), "crit": crit[:n].copy(),
+           "cg_its": its[:n].astype(np.int64), "cg_info": info[:n].astype(np.int64),
+           "phi_t0": st.phi_t0, "phi_nloc": st.phi_nloc, "ms_create": st.ms_create, "ms_loop": st.ms_loop,
+           "ms_flow": st.ms_flow, "alg_bytes_per_iter": st.alg_bytes_per_iter,
+           "cg_iters_total": int(st.bb.cg_iters_total), "cg_redo": int(st.bb.cg_redo),
+           "kernels": {name: {"n": int(st.bb.n_k[i]), "ms": float(st.bb.ms_k[i]), "bytes": float(st.bb.bytes_k[i])}
+                       for i, name in enumerate(_lib.K_NAMES) if st.bb.n_k[i] > 0}}
+    if want_phi:
+        rep["phi"] = phi[:st.phi_nloc * nxy].copy()
+    return u, v, m, rep
 
 
 def _run(s, max_it, convergence_tol, cb, stats):

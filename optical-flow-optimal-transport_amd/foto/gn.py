@@ -39,6 +39,20 @@ def solve(f1, f2, w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
     return u, v, m, info, its.value
 
 
+def solve_ex(f1, f2, w, h, alpha, lam, rtol=GN_RTOL, maxiter=GN_MAXITER):
+    """foto_gn_solve_ex (include/foto.h): solve() with the per-solve report -- returns
+    (u, v, m, stats) with stats = {iterations, info, plan_reused, levels, ms_setup, ms_pcg,
+    ms_total, alg_bytes_per_iter}."""
+    from ._lib import GNStats
+    n = w * h
+    a, b = f64(f1, n, "f1"), f64(f2, n, "f2")
+    u, v, m = np.empty(n), np.empty(n), np.empty(n)
+    st = GNStats()
+    check(lib().foto_gn_solve_ex(dptr(a), dptr(b), w, h, float(alpha), float(lam), float(rtol), int(maxiter),
+                                 dptr(u), dptr(v), dptr(m), ctypes.byref(st)))
+    return u, v, m, {f: getattr(st, f) for f, _ in GNStats._fields_}
+
+
 class Plan:
     """A reusable GN solver for one (w, h, alpha, lambda): classical.GLLOpticalFlow after
     setAlpha/setLambda (classical.py:25-66).  Buffers, the multigrid hierarchy and the replayed

@@ -12,7 +12,9 @@ skip markers (run.sh:98-117, 135-154), same hyper-parameters (run.sh:103, 114):
 Differences from run.sh, all deliberate:
   * Sequences are independent jobs.  ``--gpus N`` starts N worker processes, one per GPU
     (HIP_VISIBLE_DEVICES=i).  Worker i takes the sequences at positions i, i+N, ... of
-    the sorted (dataset, sequence) list.  Under torch.distributed.run the RANK /
+    the sorted (dataset, sequence) list.  ``--devices LIST`` (or FOTO_RUN_DEVICES=LIST, e.g.
+    ``0,0,1,1``) maps worker i to device LIST[i mod len]: several workers can share a GPU, so
+    one solve's latency-bound serial kernels overlap another's bandwidth-bound ones.  Under torch.distributed.run the RANK /
     WORLD_SIZE / LOCAL_RANK environment picks the shard instead.  No collective is
     involved: the workers share nothing but the file system.
   * Each worker runs main.py in-process (main.main(argv)), one HIP context per worker,
@@ -383,15 +385,31 @@ def run(args):
     if args.gpus <= 1:
         rc = worker(args, 0, 1, -1)
     else:
-        # one child per GPU; this process never touches the device
+        # one child per worker; this process never touches the device
+        devs = worker_devices(args)
         procs = []
         for i in range(args.gpus):
-            env = dict(os.environ, HIP_VISIBLE_DEVICES=str(i))
+            env = dict(os.environ, HIP_VISIBLE_DEVICES=str(devs[i % len(devs)]))
             procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "run", f"--gpus={args.gpus}",
                                            f"--worker-rank={i}", *forward_args(args)], env=env))
         rc = max(p.wait() for p in procs)
     summarize(args)
     return rc
+
+
+def worker_devices(args):
+    """The device of each worker: --devices / FOTO_RUN_DEVICES (a comma list, worker i on entry
+    i mod len), else worker i on device i."""
+    spec = args.devices or os.environ.get("FOTO_RUN_DEVICES", "")
+    if not spec.strip():
+        return list(range(args.gpus))
+    try:
+        devs = [int(x) for x in spec.split(",") if x.strip() != ""]
+    except ValueError:
+        raise SystemExit(f"--devices / FOTO_RUN_DEVICES wants a comma list of device ordinals, got {spec!r}")
+    if not devs or min(devs) < 0:
+        raise SystemExit(f"--devices / FOTO_RUN_DEVICES wants a comma list of device ordinals, got {spec!r}")
+    return devs
 
 
 def forward_args(args):
@@ -405,7 +423,10 @@ def forward_args(args):
 def build_parser():
     p = argparse.ArgumentParser(description="batch pipeline (run.sh)")
     p.add_argument("command", nargs="?", default="run", choices=["download", "install", "prepare", "restart", "run"])
-    p.add_argument("--gpus", type=int, default=1, help="worker processes, one per GPU")
+    p.add_argument("--gpus", type=int, default=1, help="worker processes, one per GPU (see --devices)")
+    p.add_argument("--devices", default=None,
+                   help="comma list of device ordinals, worker i on entry i mod len (default: worker i on "
+                        "device i; env FOTO_RUN_DEVICES); e.g. --gpus 2 --devices 0,0: two workers share GPU 0")
     p.add_argument("--data", default="data")
     p.add_argument("--results", default="results")
     p.add_argument("--dataset", action="append", help="extra dataset NAME=FRAMES_DIR[:GT_DIR]")

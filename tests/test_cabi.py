@@ -63,3 +63,24 @@ def test_struct_layouts():
     # foto_bb_opts: int,int,double,int,int,int,(pad),void*,int,int
     assert ctypes.sizeof(_lib.BBOpts) == 48
     assert _lib.BBStats.n_k.offset == 56
+    assert ctypes.sizeof(_lib.BBStats) == 256
+    # foto_bb_solve_stats: int cap, 3 pointers, 4 ints, 4 doubles, then foto_bb_stats
+    assert _lib.BBSolveStats.ms_create.offset == 48 and _lib.BBSolveStats.bb.offset == 80
+    assert ctypes.sizeof(_lib.BBSolveStats) == 336
+    assert ctypes.sizeof(_lib.GNStats) == 48 and _lib.GNStats.ms_setup.offset == 16
+
+
+def test_solve_ex_argument_errors_without_gpu():
+    """foto_bb_solve_ex keeps the reference's max_it = 0 failure (benamou_brenier.py:271: phi is
+    unbound) as FOTO_ERR_STATE before touching a device, and Nt < 2 as FOTO_ERR_ARG."""
+    from foto import _lib
+    L = _lib.lib()
+    z = np.zeros(12)
+    st = _lib.BBSolveStats()
+    null = _lib._D()
+    rc = L.foto_bb_solve_ex(_lib.dptr(z), _lib.dptr(z), 4, 4, 3, 1.0, 0.3, 1e-3, 0, None, null, null, null, null,
+                            st)
+    assert rc == _lib.FOTO_ERR_STATE
+    rc = L.foto_bb_solve_ex(_lib.dptr(z), _lib.dptr(z), 1, 4, 3, 1.0, 0.3, 1e-3, 5, None, null, null, null, null,
+                            st)
+    assert rc == _lib.FOTO_ERR_ARG

@@ -143,3 +143,40 @@ def test_batch_standin(tmp_path):
         for name in ("diff.png", "gn.flo", "foto.flo", "gn.png", "foto.png", "gn.rec.png", "foto.lum.png",
                      ".out.gn.sucess", ".out.foto.sucess"):
             assert (d / name).is_file(), (seq, name)
+
+
+def _batch(tmp_path, name, *extra):
+    out = tmp_path / name
+    js = tmp_path / f"{name}.json"
+    p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "batch_bench.py"), f"--out={out}",
+                        f"--json={js}", *extra], capture_output=True, text=True, timeout=300)
+    print(p.stdout[-3000:], p.stderr[-3000:])
+    assert p.returncode == 0
+    return out, json.load(open(js)), p.stdout
+
+
+def test_batch_two_workers_share_one_gpu(tmp_path):
+    """Config 5's machinery with more than one worker (run.py --gpus 2 --devices 0,0: two worker
+    processes on this one GPU, sequences dealt i, i+2, ...): every sequence's .flo is
+    bit-identical to the single-worker run's, both workers report, and a second run over the
+    same results is a no-op (run.sh's .out.<algo>.sucess markers: nothing re-solved, no .flo
+    rewritten)."""
+    seqs = ["Dimetrodon", "Grove2", "Venus", "RubberWhale"]
+    one, r1, _ = _batch(tmp_path, "one", "--seqs=4", "--gpus=1")
+    two, r2, _ = _batch(tmp_path, "two", "--seqs=4", "--gpus=2", "--devices=0,0")
+    assert r1["rc"] == 0 and r2["rc"] == 0 and len(r2["rows"]) == 8
+    workers = sorted(f for f in os.listdir(two / "results") if f.startswith(".worker"))
+    assert workers == [".worker0.json", ".worker1.json"]
+    assert [json.load(open(two / "results" / w))["sequences"] for w in workers] == [2, 2]
+    for seq in seqs:
+        for algo in ("gn", "foto"):
+            a = (one / "results" / "synthetic" / seq / f"{algo}.flo").read_bytes()
+            b = (two / "results" / "synthetic" / seq / f"{algo}.flo").read_bytes()
+            assert a == b, (seq, algo)
+    for r in r2["rows"]:
+        if r["algo"] == "foto":
+            assert r["outer_its"] and r["iters_per_s"] > 0
+    mt = {s: os.path.getmtime(two / "results" / "synthetic" / s / "foto.flo") for s in seqs}
+    _, r3, log = _batch(tmp_path, "two", "--seqs=4", "--gpus=2", "--devices=0,0", "--reuse")
+    assert log.count("skipped (markers present)") == 4
+    assert {s: os.path.getmtime(two / "results" / "synthetic" / s / "foto.flo") for s in seqs} == mt

@@ -8,16 +8,18 @@
   Dimetrodon's 584x388) and the full 584x388x32 grid (mode 2 vs the literal stencil CG, true
   residual).
 * C3: GN at 640x480 against the reference's SuperLU solve (gn_c3.npz) and its own residual.
-* C4 size 1024x1024x64 on one device: the default spectral CG against the literal stencil CG
-  and its true residual, and the 8-shard decomposition of the 8-GPU config through the
-  transfer lists RCCL executes (no reference golden: the reference needs hours per outer
+* C4 size 1024x1024x64 on one device: the default Gauss-compressed CG (cg_mode 3) and the
+  spectral s-step CG (mode 2) against the literal stencil CG, their true residuals, and the
+  8-shard decomposition of the 8-GPU config (both spectral modes) through the transfer lists
+  RCCL executes (no reference golden: the reference needs hours per outer
   iteration at this size; the stencil CG is the reference's algorithm, tested against the
   goldens at the smaller sizes).
 
 Bars (float64), set ~30x above what the MI355X measured (printed with -s):
   * CG counts +-1 (a residual norm can land within rounding of atol);
-  * bench grid: crit 1e-8 relative, phi 1e-8 of max|phi|, flow 1e-7 px (measured, default
-    s-step CG: 2.6e-10 / 3.2e-10 / 3.1e-9; stencil CG: 4e-14 / 1e-13 / 4.6e-13);
+  * bench grid: crit 1e-8 relative, phi 1e-8 of max|phi|, flow 1e-7 px (measured, s-step CG:
+    2.6e-10 / 3.2e-10 / 3.1e-9; stencil CG: 4e-14 / 1e-13 / 4.6e-13; the default Gauss CG
+    is printed with -s);
   * C2-shaped golden: crit 1e-8, phi 1e-8, flow 1e-8 px (measured <= 2.6e-10 / 1.4e-10);
   * C2 full size, spectral vs stencil: crit 1e-8, phi 1e-8 (measured 3.3e-10 / 1.3e-10);
   * true residuals <= 1.01 rtol ||F|| (scipy's rule is on the recursive residual);
@@ -76,8 +78,9 @@ def test_metric_grid_vs_reference(gold, mode):
 
 @pytest.mark.parametrize("mode", [3, 2])
 def test_metric_grid_true_residual_ten_outer(mode):
-    """The default path (spectral s-step CG: deferred, late-planned passes, the interval
-    adapted from the previous right-hand side) solves A phi = F to scipy's rule on every
+    """The default path (mode 3: scipy's recurrence on the Gauss-compressed measure, two outer
+    iterations in flight) and the spectral s-step CG (mode 2: deferred, late-planned passes, the
+    interval adapted from the previous right-hand side) solve A phi = F to scipy's rule on every
     outer iteration, not just the first: ||F - A phi|| <= 1.01 rtol ||F|| for ten outer
     iterations run one call at a time, and the same crit sequence as one iterate(10) call
     (which enqueues each next RHS before waiting: the early-head path)."""
@@ -196,9 +199,10 @@ def test_gn_c3_vs_reference(gold):
 
 def test_c4_full_size():
     """C4 size 1024x1024x64 (BASELINE configs[3]) on one device, two outer iterations: the
-    default spectral s-step CG (Nt = 64: the t axis by the strided FFT) against the literal
-    stencil CG, the true residual of each default solve, and 8 in-process shards -- the
-    8-GPU decomposition, 8 planes and 128 rows per rank -- against the single shard."""
+    spectral s-step CG (mode 2; Nt = 64: the t axis by the strided FFT) and the default
+    Gauss-compressed CG (mode 3) against the literal stencil CG, the true residual of each
+    spectral solve, and 8 in-process shards -- the 8-GPU decomposition, 8 planes and 128 rows
+    per rank -- against the single shard, in both spectral modes."""
     Nt, Nx, Ny, r, eps = 64, 1024, 1024, 1.0, 1e-2
     rho0, rhoT = translating_gaussian(Nx, Ny)
     out = {}

@@ -155,3 +155,41 @@ def test_phase_events_only_with_timing(gold, monkeypatch, klim):
     assert a["stats"]["cg_redo"] == c["stats"]["cg_redo"]
     assert c["stats"]["ms_cg"] > 0 and a["stats"]["ms_cg"] == 0
     np.testing.assert_allclose(a["crit"], d["crit"], rtol=1e-5, atol=0)
+
+
+def test_callback_sees_its_own_iteration(gold, monkeypatch):
+    """The iteration callback runs while iteration i + 1 is already on the stream.  In the
+    pipelined loop phi(), state() and flow() called from it return iteration i's results (the
+    record of the iteration in flight keeps them): each equals the final state of a run of
+    i + 1 iterations.  The one-in-flight loop (FOTO_PIPE=0) refuses them there."""
+    d = gold("bb_tex.npz")
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, _, eps, _ = d["params"]
+    for k in ("FOTO_PIPE", "FOTO_GQ_KLIM"):
+        monkeypatch.delenv(k, raising=False)
+    seen = {}
+    with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps) as s:
+        def cb(i, crit, its, info):
+            seen[i] = (s.phi(), s.state(), s.flow())
+        s.iterate(5, 0.0, False, callback=cb)
+    assert sorted(seen) == list(range(5))
+    for n in (2, 4, 5):
+        with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps) as s:
+            s.iterate(n, 0.0, False)
+            ref = (s.phi(), s.state(), s.flow())
+        phi, (mu, q), fl = seen[n - 1]
+        assert np.array_equal(phi, ref[0])
+        assert np.array_equal(mu, ref[1][0]) and np.array_equal(q, ref[1][1])
+        for x, y in zip(fl, ref[2]):
+            assert np.array_equal(x, y)
+    monkeypatch.setenv("FOTO_PIPE", "0")
+    errs = []
+    with BBSolver(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, reg_epsilon=eps) as s:
+        def cb0(i, crit, its, info):
+            try:
+                s.phi()
+            except foto.FotoError as e:
+                errs.append(i)
+        s.iterate(3, 0.0, False, callback=cb0)
+        s.phi()   # after the call: fine
+    assert errs == [0, 1]   # (the last callback runs with nothing in flight)

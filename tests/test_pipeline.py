@@ -253,3 +253,36 @@ def test_worker_argv_round_trip(tmp_path):
                                             "--dataset=m2=/x/frames:/x/gt", "--", "--cg-mode=2"])
     b = pipeline.parse_args(["run", "--gpus=4", "--worker-rank=3", *pipeline.forward_args(a)])
     assert (b.data, b.results, b.dataset, b.extra, b.worker_rank) == (a.data, a.results, a.dataset, ["--cg-mode=2"], 3)
+
+
+def test_worker_device_map(tmp_path, monkeypatch):
+    """--devices / FOTO_RUN_DEVICES put worker i on device LIST[i mod len] (several workers can
+    share a GPU); without them worker i gets device i.  The parent only starts the children
+    (HIP_VISIBLE_DEVICES per child) and never touches a device."""
+    started = []
+
+    class FakePopen:
+        def __init__(self, cmd, env=None, **kw):
+            started.append((cmd, env["HIP_VISIBLE_DEVICES"]))
+
+        def wait(self):
+            return 0
+
+    monkeypatch.setattr(pipeline.subprocess, "Popen", FakePopen)
+    monkeypatch.setattr(pipeline, "summarize", lambda args: [])
+    monkeypatch.delenv("FOTO_RUN_DEVICES", raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    common = [f"--data={tmp_path / 'd'}", f"--results={tmp_path / 'r'}"]
+    assert pipeline.main(["run", "--gpus=3", *common]) == 0
+    assert [d for _, d in started] == ["0", "1", "2"]
+    assert [c[c.index("run") + 2] for c, _ in started] == ["--worker-rank=0", "--worker-rank=1", "--worker-rank=2"]
+    started.clear()
+    assert pipeline.main(["run", "--gpus=4", "--devices=0,0,1", *common]) == 0
+    assert [d for _, d in started] == ["0", "0", "1", "0"]
+    started.clear()
+    monkeypatch.setenv("FOTO_RUN_DEVICES", "5,5")
+    assert pipeline.main(["run", "--gpus=2", *common]) == 0
+    assert [d for _, d in started] == ["5", "5"]
+    monkeypatch.setenv("FOTO_RUN_DEVICES", "a,b")
+    with pytest.raises(SystemExit):
+        pipeline.main(["run", "--gpus=2", *common])
