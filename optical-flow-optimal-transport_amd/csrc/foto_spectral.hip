@@ -790,10 +790,10 @@ __device__ __forceinline__ void dft_reg(double (&xr)[R], double (&xi)[R]) {
 
 // stage 1 (in place on the LDS lines): for each (line, j2): the length-M1 DFT of
 // z[M2 j1 + j2] (dft_reg), times e^{-+2 pi i j2 k1 / M}, stored at row k1, column j2
-template <int M1, int M2, bool INV, int LPB>
+template <int M1, int M2, bool INV, int LPB, int NTH = 256>
 __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
     constexpr int LS = FftGeom<M1, M2>::LS;
-    for (int task = threadIdx.x; task < LPB * M2; task += 256) {
+    for (int task = threadIdx.x; task < LPB * M2; task += NTH) {
         const int l = task / M2, j2 = task - (task / M2) * M2;
         double* Ll = L + l * LS;
         double xr[M1], xi[M1];
@@ -815,10 +815,10 @@ __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
 
 // stage 2 (in place): for each (line, k1): the length-M2 DFT of row k1; element
 // k = k1 + M1 k2 of the result lands at row k1, column k2
-template <int M1, int M2, bool INV, int LPB>
+template <int M1, int M2, bool INV, int LPB, int NTH = 256>
 __device__ __forceinline__ void fft_stage2(double* L) {
     constexpr int LS = FftGeom<M1, M2>::LS;
-    for (int task = threadIdx.x; task < LPB * M1; task += 256) {
+    for (int task = threadIdx.x; task < LPB * M1; task += NTH) {
         const int l = task / M1, k1 = task - (task / M1) * M1;
         double* Lr = L + l * LS + 2 * (M2 + 1) * k1;
         double xr[M2], xi[M2];
@@ -851,14 +851,16 @@ __device__ __forceinline__ void fft_stage2(double* L) {
 template <int P>
 struct LdsPrime { static constexpr bool value = P > 32; };
 
-template <int M1, int P, bool INV, int LPB>
+template <int M1, int P, bool INV, int LPB, int NTH = 256>
 __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
     constexpr int LS = FftGeom<M1, P>::LS;
     constexpr int H = (P - 1) / 2;
     constexpr int ROWS = LPB * M1;
     constexpr int KS = H / 4, NTL = (H + 1 + 15) / 16, MT = ROWS / 8;
+    constexpr int NW = NTH / 64;   // waves of the block (the M tiles are dealt to them)
     static_assert(H % 4 == 0 && ROWS % 8 == 0, "prime stage: K steps of 4, M tiles of 8 rows");
-    for (int task = threadIdx.x; task < ROWS * H; task += 256) {   // u, v in place
+    static_assert(NTH % 64 == 0, "whole waves");
+    for (int task = threadIdx.x; task < ROWS * H; task += NTH) {   // u, v in place
         const int row = task / H, j = 1 + task - row * H;
         const int l = row / M1, k1 = row - l * M1;
         double* Lr = L + l * LS + 2 * (P + 1) * k1;
@@ -871,13 +873,13 @@ __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int am = lane & 15, ak = lane >> 4;   // A operand: row am, k ak of the step
-    constexpr int MTW = (MT + 3) / 4;           // M tiles per wave
+    constexpr int MTW = (MT + NW - 1) / NW;     // M tiles per wave
     dbl4 dc[MTW][NTL], ds[MTW][NTL];
     double z0r[MTW][2], z0i[MTW][2];
 #pragma unroll
     for (int w = 0; w < MTW; ++w) {
-        const int mt = wave + 4 * w;
-        if (MT % 4 != 0 && mt >= MT) continue;
+        const int mt = wave + NW * w;
+        if (MT % NW != 0 && mt >= MT) continue;
         // this lane's A row: complex row 8 mt + (am & 7), real (am < 8) or imaginary part
         const int rowa = 8 * mt + (am & 7);
         const int offa = (rowa / M1) * LS + 2 * (P + 1) * (rowa % M1) + (am >> 3);
@@ -913,8 +915,8 @@ __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < MTW; ++w) {
-        const int mt = wave + 4 * w;
-        if (MT % 4 != 0 && mt >= MT) continue;
+        const int mt = wave + NW * w;
+        if (MT % NW != 0 && mt >= MT) continue;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = 8 * mt + (lane >> 4) + 4 * h;
@@ -942,10 +944,10 @@ __device__ __forceinline__ void fft_stage2_prime(double* L, const double* CS) {
 }
 
 // the stage-2 variant for row length M2, and the LDS root table it needs (doubles)
-template <int M1, int M2, bool INV, int LPB>
+template <int M1, int M2, bool INV, int LPB, int NTH = 256>
 __device__ __forceinline__ void fft_stage2_any(double* L, const double* CS) {
-    if constexpr (LdsPrime<M2>::value) fft_stage2_prime<M1, M2, INV, LPB>(L, CS);
-    else fft_stage2<M1, M2, INV, LPB>(L);
+    if constexpr (LdsPrime<M2>::value) fft_stage2_prime<M1, M2, INV, LPB, NTH>(L, CS);
+    else fft_stage2<M1, M2, INV, LPB, NTH>(L);
 }
 template <int M2>
 constexpr int fft_cs_len() { return LdsPrime<M2>::value ? 2 * M2 : 2; }
@@ -1249,6 +1251,387 @@ static hipError_t dct_fft_axis(int outer, int n, int inner, bool inv, const doub
     }
     FOTO_FFT_SIZES(FOTO_FFT_LAUNCH)
 #undef FOTO_FFT_LAUNCH
+    return hipErrorNotSupported;
+}
+
+// ============================================================================ x and t axes in one pass
+//
+// A single shard's 3-D DCT is separable, and DCTs along different axes commute, so the solve's
+// forward transform can run as (x, t) then y instead of x, y, t: one block per row y takes the
+// Nt lines (t, y, :) through the x-axis FFT DCT above (XT_LPB line images in LDS at a time) and
+// folds each finished pair of lines (j, Nt - 1 - j) into the t-axis DCT of its columns the way
+// the column kernels do (thread kx: e_m += E[m][j] (x_j + x_{Nt-1-j}), o_m += O[m][j] (x_j -
+// x_{Nt-1-j}), j ascending -- TCol's even / odd halves in Cth, the same sums in the same order).
+// The x-transformed volume never goes to HBM: the chain is two full-volume passes instead of
+// three, and the output is in the layout the plain y pass expects ([kt][y][kx]), which then
+// leaves b^ exactly where the histogram and x^ read it.  The inverse mirrors it: the y pass,
+// then one block per row y loads its columns x^[kt][y][kx], forms the inverse t-DCT of a chunk
+// of line pairs in registers, stages those lines in LDS and runs the x-axis inverse on them.
+// MEASURED SLOWER, so opt-in (FOTO_DCT_XT=1, SpectralPlan::init): 151 / 165 us per launch at the
+// bench grid against 69 / 72 us for the pairs of passes it replaces -- the slab's state pins
+// one block per CU and its phases serialise; the passes are latency-bound, not HBM-bound (their
+// intermediates stay in the Infinity Cache), so removing one saves less than it costs here.
+// Single shard, Nt even and <= 32 (the column kernels' sizes), 64 <= Nx <= 640 with an FFT plan.
+// A block carries the whole x-transformed row slab's t-sums (Nt x Nx values, 164 KB at the bench
+// grid) through the line loop: 512 threads (two waves per SIMD, 256 VGPRs each -- 640 threads
+// would leave 168 and spill), thread kx owning column kx's sums, the even half in registers and
+// the odd half in LDS (read, advanced by the chunk's pairs and written back once per chunk, so
+// neither is live in registers beside the FFT stages' codelets: both in registers spilled ~68
+// VGPRs).  The columns beyond 512 (Nx = 584, 640) are split four ways, part p of column
+// 512 + tid / 4 taking the sums m = p, p + 4, ... of both halves in registers.  The sums run over
+// j in ascending order as in the column kernels.
+constexpr int XT_MAXH = 16;   // Nt <= 2 XT_MAXH
+constexpr int XT_NTH = 512;
+constexpr int XT_SPLIT = 4;   // parts of a column beyond XT_NTH
+constexpr int XT_MAXN = XT_NTH + XT_NTH / XT_SPLIT;   // 640
+constexpr int XT_HB = XT_MAXH / XT_SPLIT;             // sums of a part
+template <int M1, int M2>
+struct XtGeom {
+    static constexpr int M = M1 * M2, N = 2 * M;
+    static constexpr int LS = FftGeom<M1, M2>::LS;
+    static constexpr int LPBF = 16;                    // forward: lines per chunk (8 pairs)
+    static constexpr int LPBI = 8;                     // inverse: lines per chunk (+ their X rows)
+    static constexpr int NB = N > XT_NTH ? N - XT_NTH : 1;   // split columns (>= 1: array sizes)
+};
+
+// line slot l of chunk q (pairs q PP .. q PP + PP - 1): slot 2 i is t = j, slot 2 i + 1 is
+// t = Nt - 1 - j, j = q PP + i
+__device__ __forceinline__ int xt_line_t(int q, int pp, int nt, int l) {
+    const int j = q * pp + (l >> 1);
+    return (l & 1) ? nt - 1 - j : j;
+}
+
+// X_kx of a line from its DFT image (k_dct_fft_fwd's output phase for one column)
+struct XtCol {
+    int pa, pb;
+    double war, wai, wbr, wbi, sk;
+    bool hi;
+    template <int M1, int M2>
+    __device__ __forceinline__ void init(const double* PA, const double* PB, int kx) {
+        constexpr int M = M1 * M2, N = 2 * M;
+        hi = kx > M;
+        const int k = hi ? N - kx : kx;
+        pa = 2 * fft_pos<M1, M2>(k == M ? 0 : k);
+        pb = 2 * fft_pos<M1, M2>(k == 0 ? 0 : M - k);
+        war = PA[2 * k];
+        wai = PA[2 * k + 1];
+        wbr = PB[2 * k];
+        wbi = PB[2 * k + 1];
+        const double s0 = PB[2 * (M + 1)], s = PB[2 * (M + 1) + 1];
+        sk = hi ? -s : (k == 0 ? s0 : s);
+    }
+    __device__ __forceinline__ double x(const double* Ll) const {
+        const double zr = Ll[pa], zi = Ll[pa + 1], cr = Ll[pb], ci = -Ll[pb + 1];
+        const double er = 0.5 * (zr + cr), ei = 0.5 * (zi + ci);
+        const double orr = 0.5 * (zi - ci), oi = 0.5 * (cr - zr);
+        const double vr = er + fma(war, orr, -wai * oi), vi = ei + fma(war, oi, wai * orr);
+        const double yr = fma(wbr, vr, -wbi * vi), yi = fma(wbr, vi, wbi * vr);
+        return sk * (hi ? yi : yr);
+    }
+};
+
+template <int M1, int M2>
+__global__ __launch_bounds__(XT_NTH) void k_dct_xt_fwd(int Nt, int Ny, const double* __restrict__ tab,
+                                                       const double* __restrict__ Ch, const double* __restrict__ in,
+                                                       double* __restrict__ out) {
+    using G = XtGeom<M1, M2>;
+    constexpr int M = G::M, N = G::N, NTH = XT_NTH, LS = G::LS, LPB = G::LPBF, PP = LPB / 2;
+    static_assert(N <= XT_MAXN, "columns beyond 512 split four ways: Nx <= 640");
+    __shared__ double L[LPB * LS];
+    __shared__ double OS[XT_MAXH][XT_NTH];   // part A's odd sums, [m][column]
+    __shared__ double CS[fft_cs_len<M2>()];
+    const int tid = threadIdx.x, y = blockIdx.x;
+    const int H = Nt / 2;
+    if constexpr (LdsPrime<M2>::value)
+        for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
+    const double* TW = tab;
+    const double* PA = tab + 2 * M;
+    const double* PB = PA + 2 * (M + 1);
+    // part A: column tid, all sums; part B (Nx > 512): column 512 + tid / 4, sums m = p + 4 i
+    const bool ha = tid < N;
+    const int cb = XT_NTH + tid / XT_SPLIT, pb = tid % XT_SPLIT;
+    const bool hb = (N > XT_NTH) && cb < N;
+    double e[XT_MAXH], eb[XT_HB], ob[XT_HB];
+#pragma unroll
+    for (int m = 0; m < XT_MAXH; ++m) {
+        e[m] = 0.0;
+        OS[m][tid] = 0.0;   // (a thread only ever touches its own column's slots)
+    }
+#pragma unroll
+    for (int i = 0; i < XT_HB; ++i) { eb[i] = 0.0; ob[i] = 0.0; }
+    const int nq = (H + PP - 1) / PP;
+    for (int q = 0; q < nq; ++q) {
+        const int npair = min(PP, H - q * PP), nl = 2 * npair;
+        {   // the chunk's lines into LDS in Makhoul order (all loads issued first); a thread takes
+            // columns tid + NTH c of every line, so its LDS positions are the same in every line
+            // and chunk (an index decomposition per element was hoisted out of the chunk loop and
+            // spilled)
+            constexpr int CPL = (N + NTH - 1) / NTH;
+            double xv[LPB][CPL];
+#pragma unroll
+            for (int l = 0; l < LPB; ++l) {
+                const double* row = in + ((int64_t)xt_line_t(q, PP, Nt, l) * Ny + y) * N;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const int j = tid + NTH * c;
+                    xv[l][c] = (l < nl && (N % NTH == 0 || j < N)) ? ld_dead(&row[j]) : 0.0;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = tid + NTH * c;
+                if (N % NTH != 0 && j >= N) continue;
+                const int p = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+                const int pos = 2 * fft_zpos<M2>(p >> 1) + (p & 1);
+#pragma unroll
+                for (int l = 0; l < LPB; ++l) L[l * LS + pos] = xv[l][c];
+            }
+        }
+        __syncthreads();
+        fft_stage1<M1, M2, false, LPB, NTH>(L, TW);
+        __syncthreads();
+        fft_stage2_any<M1, M2, false, LPB, NTH>(L, CS);
+        __syncthreads();
+        double od[XT_MAXH];   // part A's odd sums while this chunk's pairs are added
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) od[m] = OS[m][tid];
+        // (the columns' twiddles are re-read per chunk, L1 hits: held across the FFT stages they
+        // cost ~26 VGPRs)
+        XtCol A, B;
+        if (ha) A.init<M1, M2>(PA, PB, tid);
+        if (hb) B.init<M1, M2>(PA, PB, cb);
+        for (int i = 0; i < npair; ++i) {   // pair j = q PP + i: lines t = j (slot 2 i), Nt - 1 - j
+            const int j = q * PP + i;
+            const double* L0 = L + (2 * i) * LS;
+            const double* L1 = L0 + LS;
+            if (ha) {
+                const double x0 = A.x(L0), x1 = A.x(L1);
+                const double sv = x0 + x1, dv = x0 - x1;
+#pragma unroll
+                for (int m = 0; m < XT_MAXH; ++m) {
+                    if (m < H) {
+                        e[m] = fma(Ch[m * H + j], sv, e[m]);
+                        od[m] = fma(Ch[H * H + m * H + j], dv, od[m]);
+                    }
+                }
+            }
+            if (hb) {
+                const double x0 = B.x(L0), x1 = B.x(L1);
+                const double sv = x0 + x1, dv = x0 - x1;
+#pragma unroll
+                for (int i4 = 0; i4 < XT_HB; ++i4) {
+                    const int m = pb + XT_SPLIT * i4;
+                    if (m < H) {
+                        eb[i4] = fma(Ch[m * H + j], sv, eb[i4]);
+                        ob[i4] = fma(Ch[H * H + m * H + j], dv, ob[i4]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) OS[m][tid] = od[m];
+        __syncthreads();   // (the next chunk's lines overwrite L)
+    }
+    if (ha) {
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) {
+            if (m < H) {
+                out[((int64_t)(2 * m) * Ny + y) * N + tid] = e[m];
+                out[((int64_t)(2 * m + 1) * Ny + y) * N + tid] = OS[m][tid];
+            }
+        }
+    }
+    if (hb) {
+#pragma unroll
+        for (int i4 = 0; i4 < XT_HB; ++i4) {
+            const int m = pb + XT_SPLIT * i4;
+            if (m < H) {
+                out[((int64_t)(2 * m) * Ny + y) * N + cb] = eb[i4];
+                out[((int64_t)(2 * m + 1) * Ny + y) * N + cb] = ob[i4];
+            }
+        }
+    }
+}
+
+template <int M1, int M2>
+__global__ __launch_bounds__(XT_NTH) void k_dct_tx_inv(int Nt, int Ny, const double* __restrict__ tab,
+                                                       const double* __restrict__ Ch, const double* __restrict__ in,
+                                                       double* __restrict__ out) {
+    using G = XtGeom<M1, M2>;
+    constexpr int M = G::M, N = G::N, NTH = XT_NTH, LS = G::LS, LPB = G::LPBI, PP = LPB / 2, NB = G::NB;
+    static_assert(N <= XT_MAXN, "columns beyond 512 split four ways: Nx <= 640");
+    // L: the chunk's line images; before the input phase writes them, the split columns'
+    // partial sums PE / PO live in the same space
+    static_assert(2 * XT_SPLIT * PP * NB <= LPB * LS, "partial sums fit the line images");
+    __shared__ double L[LPB * LS];
+    __shared__ double XL[LPB * N];            // the chunk's lines after the inverse t-DCT, natural order
+    __shared__ double XO[XT_MAXH][XT_NTH];    // part A's odd inputs x^_{2m+1}, [m][column]
+    __shared__ double CS[fft_cs_len<M2>()];
+    double(*PE)[PP][NB] = reinterpret_cast<double(*)[PP][NB]>(L);
+    double(*PO)[PP][NB] = reinterpret_cast<double(*)[PP][NB]>(L + XT_SPLIT * PP * NB);
+    const int tid = threadIdx.x, y = blockIdx.x;
+    const int H = Nt / 2;
+    if constexpr (LdsPrime<M2>::value)
+        for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
+    const double* TW = tab;
+    const double* PA = tab + 2 * M;
+    const double* PB = PA + 2 * (M + 1);
+    const double is0 = 1.0 / PB[2 * (M + 1)], is = 1.0 / PB[2 * (M + 1) + 1];
+    const bool ha = tid < N;
+    const int cb = XT_NTH + tid / XT_SPLIT, pb = tid % XT_SPLIT;
+    const bool hb = (N > XT_NTH) && cb < N;
+    double xe[XT_MAXH], xeb[XT_HB], xob[XT_HB];   // x^_{2m}, x^_{2m+1} (all loads first)
+    {
+        double xo[XT_MAXH];
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) {
+            xe[m] = (m < H && ha) ? ld_dead(&in[((int64_t)(2 * m) * Ny + y) * N + tid]) : 0.0;
+            xo[m] = (m < H && ha) ? ld_dead(&in[((int64_t)(2 * m + 1) * Ny + y) * N + tid]) : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) XO[m][tid] = xo[m];   // (own column's slots only)
+    }
+#pragma unroll
+    for (int i4 = 0; i4 < XT_HB; ++i4) {
+        const int m = pb + XT_SPLIT * i4;
+        xeb[i4] = (m < H && hb) ? ld_dead(&in[((int64_t)(2 * m) * Ny + y) * N + cb]) : 0.0;
+        xob[i4] = (m < H && hb) ? ld_dead(&in[((int64_t)(2 * m + 1) * Ny + y) * N + cb]) : 0.0;
+    }
+    const int nq = (H + PP - 1) / PP;
+    for (int q = 0; q < nq; ++q) {
+        const int npair = min(PP, H - q * PP), nl = 2 * npair;
+        double xo[XT_MAXH];   // part A's odd inputs for this chunk's sums
+#pragma unroll
+        for (int m = 0; m < XT_MAXH; ++m) xo[m] = XO[m][tid];
+        for (int i = 0; i < npair; ++i) {   // k_dct_t_inv_xhat's sums for t = j, Nt - 1 - j
+            const int j = q * PP + i;
+            if (ha) {
+                double ev = 0.0, ov = 0.0;
+#pragma unroll
+                for (int m = 0; m < XT_MAXH; ++m) {
+                    if (m < H) {
+                        ev = fma(Ch[m * H + j], xe[m], ev);
+                        ov = fma(Ch[H * H + m * H + j], xo[m], ov);
+                    }
+                }
+                XL[(2 * i) * N + tid] = ev + ov;
+                XL[(2 * i + 1) * N + tid] = ev - ov;
+            }
+            if (hb) {
+                double ev = 0.0, ov = 0.0;
+#pragma unroll
+                for (int i4 = 0; i4 < XT_HB; ++i4) {
+                    const int m = pb + XT_SPLIT * i4;
+                    if (m < H) {
+                        ev = fma(Ch[m * H + j], xeb[i4], ev);
+                        ov = fma(Ch[H * H + m * H + j], xob[i4], ov);
+                    }
+                }
+                PE[pb][i][cb - XT_NTH] = ev;
+                PO[pb][i][cb - XT_NTH] = ov;
+            }
+        }
+        if (N > XT_NTH) {   // the split columns' lines: the four parts in order
+            __syncthreads();
+            for (int w = tid; w < npair * NB; w += NTH) {
+                const int i = w / NB, c = w - i * NB;
+                const double ev = ((PE[0][i][c] + PE[1][i][c]) + PE[2][i][c]) + PE[3][i][c];
+                const double ov = ((PO[0][i][c] + PO[1][i][c]) + PO[2][i][c]) + PO[3][i][c];
+                XL[(2 * i) * N + XT_NTH + c] = ev + ov;
+                XL[(2 * i + 1) * N + XT_NTH + c] = ev - ov;
+            }
+        }
+        __syncthreads();
+        // k_dct_fft_inv's input phase on the LDS rows: Z_k and Z_{M-k} from X_k, X_{N-k}, X_{M-k},
+        // X_{N-M+k}; thread: k = tid + NTH c of every line (the per-k twiddles once per chunk)
+        constexpr int MH = M / 2 + 1;
+        constexpr int CPK = (MH + NTH - 1) / NTH;
+#pragma unroll
+        for (int c = 0; c < CPK; ++c) {
+            const int kk = tid + NTH * c;
+            if (MH % NTH != 0 && kk >= MH) continue;
+            // V_j = e^{+i pi j/(2N)} Y_j (j = kk, M - kk), then Z_q = Ve_q + i Vo_q (q = kk, M - kk)
+            const int j1 = kk, j2 = M - kk;
+            const double s1 = (j1 == 0) ? is0 : is, s2 = (j2 == 0) ? is0 : is;
+            const double b1r = PB[2 * j1], b1i = -PB[2 * j1 + 1], b2r = PB[2 * j2], b2i = -PB[2 * j2 + 1];
+            const double a1r = PA[2 * j1], a1i = -PA[2 * j1 + 1], a2r = PA[2 * j2], a2i = -PA[2 * j2 + 1];
+            const int q1 = 2 * fft_zpos<M2>(kk), q2 = 2 * fft_zpos<M2>(M - kk);
+            const bool two = kk != 0 && 2 * kk != M;
+#pragma unroll
+            for (int l = 0; l < LPB; ++l) {
+                double z1r = 0.0, z1i = 0.0, z2r = 0.0, z2i = 0.0;
+                if (l < nl) {
+                    const double* X = XL + l * N;
+                    const double xk = X[kk], xnk = (kk != 0) ? X[N - kk] : 0.0;
+                    const double xmk = X[M - kk], xpk = (M - kk != 0) ? X[N - (M - kk)] : 0.0;
+                    const double y1r = xk * s1, y1i = (j1 == 0) ? 0.0 : -xnk * is;
+                    const double y2r = xmk * s2, y2i = (j2 == 0) ? 0.0 : -xpk * is;
+                    const double ar = fma(b1r, y1r, -b1i * y1i), ai = fma(b1r, y1i, b1i * y1r);
+                    const double br = fma(b2r, y2r, -b2i * y2i), bi = fma(b2r, y2i, b2i * y2r);
+                    {   // Z_kk from V_kk = (ar, ai), V_{M-kk} = (br, bi)
+                        const double cbi = -bi;
+                        const double er = 0.5 * (ar + br), ei = 0.5 * (ai + cbi);
+                        const double dr = 0.5 * (ar - br), di = 0.5 * (ai - cbi);
+                        const double orr = fma(a1r, dr, -a1i * di), oi = fma(a1r, di, a1i * dr);
+                        z1r = er - oi;
+                        z1i = ei + orr;
+                    }
+                    {   // Z_{M-kk} from V_{M-kk}, V_kk
+                        const double cai = -ai;
+                        const double er = 0.5 * (br + ar), ei = 0.5 * (bi + cai);
+                        const double dr = 0.5 * (br - ar), di = 0.5 * (bi - cai);
+                        const double orr = fma(a2r, dr, -a2i * di), oi = fma(a2r, di, a2i * dr);
+                        z2r = er - oi;
+                        z2i = ei + orr;
+                    }
+                }
+                L[l * LS + q1] = z1r;
+                L[l * LS + q1 + 1] = z1i;
+                if (two) {
+                    L[l * LS + q2] = z2r;
+                    L[l * LS + q2 + 1] = z2i;
+                }
+            }
+        }
+        __syncthreads();
+        fft_stage1<M1, M2, true, LPB, NTH>(L, TW);
+        __syncthreads();
+        fft_stage2_any<M1, M2, true, LPB, NTH>(L, CS);
+        __syncthreads();
+        constexpr double iM = 1.0 / M;
+        constexpr int CPL = (N + NTH - 1) / NTH;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {   // x_i = v_p, p = Makhoul position of i (i = tid + NTH c)
+            const int i = tid + NTH * c;
+            if (N % NTH != 0 && i >= N) continue;
+            const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
+            const int pos = 2 * fft_pos<M1, M2>(p >> 1) + (p & 1);
+#pragma unroll
+            for (int l = 0; l < LPB; ++l)
+                if (l < nl) out[((int64_t)xt_line_t(q, PP, Nt, l) * Ny + y) * N + i] = L[l * LS + pos] * iM;
+        }
+        __syncthreads();   // (the next chunk rewrites XL and L)
+    }
+}
+
+static bool xt_supported(int Nx, int Nt) {
+    int m1, m2;
+    return Nt % 2 == 0 && Nt >= 2 && Nt <= 2 * XT_MAXH && Nx >= 64 && Nx <= XT_MAXN && fft_factors(Nx, &m1, &m2);
+}
+
+// the fused (x, t) forward / (t, x) inverse of a single shard's [t][y][x] volume <-> [kt][y][kx]
+static hipError_t dct_xt(int Nt, int Ny, int Nx, bool inv, const double* tab, const double* Ch, const double* in,
+                         double* out, hipStream_t s) {
+#define FOTO_XT_LAUNCH(NN, A, B)                                                                              \
+    if constexpr (NN >= 64 && NN <= XT_MAXN) {                                                                \
+        if (Nx == NN) {                                                                                       \
+            if (inv) k_dct_tx_inv<A, B><<<Ny, XT_NTH, 0, s>>>(Nt, Ny, tab, Ch, in, out);                      \
+            else k_dct_xt_fwd<A, B><<<Ny, XT_NTH, 0, s>>>(Nt, Ny, tab, Ch, in, out);                          \
+            return hipGetLastError();                                                                         \
+        }                                                                                                     \
+    }
+    FOTO_FFT_SIZES(FOTO_XT_LAUNCH)
+#undef FOTO_XT_LAUNCH
     return hipErrorNotSupported;
 }
 
@@ -2782,6 +3165,7 @@ struct SpecImpl {
     int nb_ring = 0;
     double* Cth = nullptr;        // t-axis DCT-II even | odd halves (column kernels)
     bool tcol = false;            // single shard, s-step, Nt in FOTO_TCOL_SIZES
+    bool xt = false;              // single shard, Gauss CG: x and t DCTs in one pass (k_dct_xt_fwd / k_dct_tx_inv)
     int tcol_nb = 0;              // column kernels' blocks
     int last_passes = 0;          // passes of the previous s-step solve (first chunk size)
     // deferred solves in flight (solve_deferred -> finish), oldest first: one for the s-step
@@ -3026,6 +3410,15 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     // the Gauss-compressed CG needs the bin-ordered voxel list; boxes its packing does not
     // cover run the s-step CG (decided on the whole grid, so every rank agrees)
     P->gauss = gauss && gq_perm_ok(g.Nx, g.Nt * g.Ny);
+    {   // (x, t) / (t, x) in one pass: single shard, the column kernels' t sizes, an FFT x plan.
+        // Opt-in (FOTO_DCT_XT=1): correct (the whole GPU suite passes with it) but measured 2.2x
+        // slower than the two passes it replaces -- 151 / 165 us against 69 / 72 us at the bench
+        // grid (profiles/r05_xt_ab.txt): a row slab's t-sums (164 KB) pin one 512-thread block
+        // per CU, whose load / FFT / accumulate phases then run without overlap.
+        const char* e = getenv("FOTO_DCT_XT");
+        P->xt = P->gauss && P->tcol && world == 1 && P->Fx && g_dct_fft && xt_supported(g.Nx, g.Nt) &&
+                (e && atoi(e) == 1);
+    }
     if (P->gauss) {
         FOTO_TRY(P->alloc(sizeof(GqState), &b)); P->gq = (GqState*)b;
         FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
@@ -3478,14 +3871,27 @@ static int gq_enqueue(SpecImpl* P, const double* b, double* x, double rtol, int 
     const Geo& g = P->g;
     const double N = (double)g.Nt * (double)g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
-    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, P->rh, s));
-    if (P->tcol) FOTO_HIP_CHECK(launch_tcol(P, false, P->rh, nullptr, rtol, maxiter, s, TC_PLAIN));
-    else FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, (int)g.nxy, P->rh, P->bh, s));
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    if (P->xt) {   // b -(x, t)-> tmp -y-> b^: two passes (k_dct_xt_fwd)
+        FOTO_HIP_CHECK(dct_xt(g.Nt, g.Ny, g.Nx, false, P->Fx, P->Cth, b, P->tmp, s));
+        FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, P->bh, s));
+        if (kt) kt->stop(e, s, FOTO_K_DCT, 4.0 * 8.0 * N);
+    } else {
+        FOTO_HIP_CHECK(dct_pass(P, 0, false, g.Nt * g.Ny, 1, b, P->tmp, s));
+        FOTO_HIP_CHECK(dct_pass(P, 1, false, g.Nt, g.Nx, P->tmp, P->rh, s));
+        if (P->tcol) FOTO_HIP_CHECK(launch_tcol(P, false, P->rh, nullptr, rtol, maxiter, s, TC_PLAIN));
+        else FOTO_HIP_CHECK(dct_pass(P, 2, false, 1, (int)g.nxy, P->rh, P->bh, s));
+        if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+    }
     FOTO_TRY(gq_measure(P, kt, s));
     FOTO_TRY(gq_solve(P, rtol, maxiter, kt, s));
     e = kt ? kt->start(s) : nullptr;
+    if (P->xt) {   // x^ -> rh -y-> tmp -(t, x)-> x (k_dct_tx_inv)
+        FOTO_HIP_CHECK(gq_xhat(P, P->rh, s));
+        FOTO_HIP_CHECK(dct_pass(P, 1, true, g.Nt, g.Nx, P->rh, P->tmp, s));
+        FOTO_HIP_CHECK(dct_xt(g.Nt, g.Ny, g.Nx, true, P->Fx, P->Cth, P->tmp, x, s));
+        if (kt) kt->stop(e, s, FOTO_K_DCT, 6.0 * 8.0 * N);
+        return 0;
+    }
     if (P->tcol) {
         FOTO_HIP_CHECK(launch_tcol(P, true, nullptr, P->tmp, rtol, maxiter, s));   // x^ -> rh, t^-1 -> tmp
     } else {

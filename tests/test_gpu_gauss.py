@@ -114,3 +114,29 @@ def test_gauss_sharded_small_grids_match_single(Nt, Nx, Ny, vr):
     # recurrence -- and counted in cg_redo; the counts must agree either way)
     print(Nt, Nx, Ny, vr, its, "redo", redo)
     assert max(abs(a - b) for a, b in zip(its[1], its[vr])) <= 1
+
+
+@pytest.mark.parametrize("name", ["bb_c1.npz", "bb_c2s.npz"])
+def test_dct_xt_fused_opt_in(gold, monkeypatch, name):
+    """FOTO_DCT_XT=1 (opt-in, measured slower: foto_spectral.hip): the single-shard Gauss solve's
+    3-D DCT as (x, t) then y and its inverse as y then (t, x), against the default x, y, t
+    passes on the same pair -- the same transform up to rounding: CG counts equal, crit to
+    1e-10, phi to 1e-10 of max|phi| (C1 64x64x8, and the C2-shaped 146x194x4 golden whose x plan
+    has the prime 73-point stage)."""
+    from foto.synthetic import textured_pair
+    d = gold(name)
+    Nt, Ny, Nx = (int(v) for v in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    # (bb_c2s.npz holds the pair's sums only: tests/test_gpu_configs.py rebuilds it the same way)
+    rho0, rhoT = (d["rho0"], d["rhoT"]) if "rho0" in d else textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+    out = {}
+    for xt in ("0", "1"):
+        monkeypatch.setenv("FOTO_DCT_XT", xt)
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps) as s:
+            s.iterate(6, 0.0, False)
+            out[xt] = (np.array(s.cg_its), np.array(s.crit), s.phi())
+    monkeypatch.delenv("FOTO_DCT_XT")
+    (k0, c0, p0), (k1, c1, p1) = out["0"], out["1"]
+    assert np.array_equal(k0, k1)
+    np.testing.assert_allclose(c1, c0, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-10 * np.abs(p0).max())
