@@ -45,11 +45,18 @@ def make_pair(w, h, dx, dy, seed):
     return np.uint8(np.round(255 * f)), np.uint8(np.round(255 * g))
 
 
+def sequences_list(k):
+    """The first k stand-in sequences: the 8 Middlebury-2 sizes, then again with a suffix (a
+    longer batch for steady-state throughput)."""
+    return [(name if i < len(SIZES) else f"{name}_{i // len(SIZES)}", w, h)
+            for i, (name, w, h) in ((i, SIZES[i % len(SIZES)]) for i in range(k))]
+
+
 def build(root, k):
     from PIL import Image
     import utils
     frames, gt = os.path.join(root, "frames"), os.path.join(root, "gt")
-    for i, (name, w, h) in enumerate(SIZES[:k]):
+    for i, (name, w, h) in enumerate(sequences_list(k)):
         dx, dy = 0.6 + 0.25 * i, -0.4 + 0.2 * i
         a, b = make_pair(w, h, dx, dy, i)
         os.makedirs(os.path.join(frames, name), exist_ok=True)
