@@ -1,15 +1,23 @@
 #!/usr/bin/env python3
 """FOTO hot-path benchmark: Benamou-Brenier outer iterations/s on the 640x480x32 grid.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1|2|3] [--no-cpu-baseline] [--no-gn]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1|2|3] [--mode batch|sharded]
+                    [--no-cpu-baseline] [--no-gn] [--no-strong]
 
 A "step" is one outer iteration of benamou_brenier.solve (benamou_brenier.py:204-258:
 RHS + CG Poisson solve + stepB/stepC + criterion) over the synthetic 640x480x32
 translating-Gaussian pair (SURVEY.md §8(d) S-metric; r = 1, eps = 1e-2, run.sh:114
 parameters), with every input and all solver state resident in HBM.  The stop rules are
-disabled so exactly K steps run.  With N > 1 (torch.distributed.run, one process per GPU)
-the time axis is sharded into N slabs with RCCL halo exchange (strong scaling: the same
-problem on more GPUs); value = outer iterations of that one problem per second.
+disabled so exactly K steps run.  With N > 1 (torch.distributed.run, one process per GPU):
+  * --mode batch (default; "scaling": "weak"): every GPU solves its own 640x480x32 pair, as
+    run.py streams independent sequences over GPUs (config 5, run.sh:81-157); value = the outer
+    iterations of all N solves per second (whole job), the slowest rank's clock.  The same run
+    then also measures the "strong" object: ONE problem time-sharded over the N GPUs (config 4's
+    decomposition: N time slabs, the slab <-> row-box all-to-alls and halos over RCCL), its
+    outer iterations per second -- guarded by a watchdog (FOTO_BENCH_STRONG_TIMEOUT, 180 s) so
+    a stuck collective cannot cost the headline line;
+  * --mode sharded: that time-sharded strong-scaling run as the headline ("scaling": "strong").
+At N = 1 both are the single-GPU solve.
 
 At N = 1 the line also carries a "gn" object: the GN baseline (classical.py)
 solved on the GPU at 640x480 (and 320x240), and the oracle's SuperLU solve of the 640x480 pair
@@ -54,6 +62,10 @@ def parse():
     ap.add_argument("--gn-cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch HIP-event pass (roofline fields become null)")
+    ap.add_argument("--mode", choices=["batch", "sharded"], default="batch",
+                    help="N > 1: batch = one solve per GPU (weak scaling, default); sharded = one solve time-sharded "
+                         "over the N GPUs (strong scaling)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1, batch mode: skip the time-sharded side run")
     return ap.parse_args()
 
 
@@ -361,6 +373,52 @@ def survey_bytes(k):
     return (21 + 10 * k) * NX * NY * NT * 8
 
 
+def strong_side(args, rdv, rank, world, local_rank, nccl_id, rho0, rhoT):
+    """Batch mode, N > 1: ONE solve time-sharded over the N GPUs (config 4's decomposition over
+    RCCL) on the same workload: warmup, barrier, K timed outer iterations, the slowest rank's
+    clock.  A watchdog ends the process after FOTO_BENCH_STRONG_TIMEOUT s (default 180) with the
+    headline line printed by rank 0 and "strong": {"error": "timeout"} -- a collective that
+    never completes cannot cost the data-parallel measurement."""
+    import threading
+    from foto.bb import BBSolver
+    limit = float(os.environ.get("FOTO_BENCH_STRONG_TIMEOUT", "180"))
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(limit):
+            if rank == 0 and _PENDING_LINE:
+                _PENDING_LINE[0]["strong"] = {"error": f"timeout after {limit:.0f} s"}
+                print(json.dumps(_PENDING_LINE[0]), flush=True)
+            os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        with BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=local_rank, cg_mode=args.cg_mode,
+                      rank=rank, world=world, nccl_id=nccl_id) as t:
+            t.iterate(args.warmup, 0.0, stop_rules=False)
+            t.sync()
+            rdv.barrier()
+            n0 = len(t.cg_its)
+            t0 = time.perf_counter()
+            t.iterate(args.steps, 0.0, stop_rules=False)
+            t.sync()
+            el = rdv.max(time.perf_counter() - t0)
+            rdv.barrier()
+            cg = t.cg_its[n0:]
+        out = {"value": round(args.steps / el, 4), "unit": "iters/s", "ms_per_step": round(1e3 * el / args.steps, 3),
+               "steps": args.steps, "scaling": "strong", "n_gpus": world,
+               "cg_iters_per_step": round(float(np.mean(cg)), 2) if cg else None,
+               "parallelism": f"time-slab x{world}: {NT} planes split over {world} ranks, slab <-> row-box all-to-alls "
+                              f"(pipelined, phi's halo inside) and the w_t halo over RCCL (DESIGN.md 5)"}
+    except Exception as e:   # reported, not fatal: the headline is the data-parallel run
+        out = {"error": f"{type(e).__name__}: {e}"[:300]}
+    done.set()
+    return out
+
+
+_PENDING_LINE = []   # rank 0's line while the strong side run is in flight (its watchdog prints it)
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
@@ -373,27 +431,37 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # FOTO_BENCH_DEVICES=0,0: rank i on device LIST[i mod len] (tests: two batch-mode ranks on
+    # one GPU); default: the rank's own GPU
+    devs = [int(v) for v in os.environ.get("FOTO_BENCH_DEVICES", "").split(",") if v.strip()]
+    if devs:
+        local_rank = devs[local_rank % len(devs)]
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rdv = None
     nccl_id = None
+    sharded = world > 1 and args.mode == "sharded"
+    want_strong = world > 1 and args.mode == "batch" and not args.no_strong
     if world > 1:
         rdv = FileRendezvous(rank, world)
-        buf = None
-        if rank == 0:
-            import ctypes
-            import foto
-            b = ctypes.create_string_buffer(128)
-            foto._lib.check(foto.lib().foto_nccl_unique_id(b))
-            buf = bytes(b.raw)
-        nccl_id = rdv.broadcast("nccl_id", buf)
+        if sharded or want_strong:
+            buf = None
+            if rank == 0:
+                import ctypes
+                import foto
+                b = ctypes.create_string_buffer(128)
+                foto._lib.check(foto.lib().foto_nccl_unique_id(b))
+                buf = bytes(b.raw)
+            nccl_id = rdv.broadcast("nccl_id", buf)
 
     from foto.bb import BBSolver
     from foto.synthetic import translating_gaussian
 
     rho0, rhoT = translating_gaussian(NX, NY)
+    # batch mode: this rank's own solve (no RCCL); sharded mode: its slab of the one solve
     s = BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=local_rank, cg_mode=args.cg_mode,
-                 rank=rank, world=world, nccl_id=nccl_id)
+                 rank=rank if sharded else 0, world=world if sharded else 1, nccl_id=nccl_id if sharded else None)
+    solves = world if (world > 1 and not sharded) else 1   # problems the timed region advances
 
     def barrier():
         s.sync()
@@ -456,15 +524,15 @@ def main():
                     "kernel": dom, "alg_bytes_per_launch": k["bytes"] / k["n"], "avg_launch_us": round(avg_s * 1e6, 2)}
             try:
                 if dom == "spec_cg":
-                    roof.update(stream_ceiling(world, avg_s * 1e6))
-                elif dom == "prox" and world == 1:
+                    roof.update(stream_ceiling(world if sharded else 1, avg_s * 1e6))
+                elif dom == "prox" and not sharded:
                     roof.update(stream_ceiling_prox(avg_s * 1e6))
             except Exception as e:   # an older library in an A/B run (FOTO_LIB) has no probe
                 roof["stream_note"] = f"stream probe unavailable: {e}"
 
     line = None
     if rank == 0:
-        value = args.steps / elapsed
+        value = solves * args.steps / elapsed
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -474,16 +542,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (translating Gaussian pair, SURVEY.md §8(d); no Middlebury offline)",
             "config": {"workload": "FOTO Benamou-Brenier outer iteration, 640x480x32, r=1, eps=1e-2, "
                                    "CG rtol=1e-6 (scipy rule), stop rules off",
                        "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral-cg", "spectral-sstep8", "spectral-gauss"][args.cg_mode],
-                       "parallelism": f"time-slab x{world}" if world > 1 else "single GPU"},
+                       "parallelism": (f"time-slab x{world} (one solve over {world} GPUs, RCCL)" if sharded else
+                                       f"data-parallel x{world} (one solve per GPU, independent pairs as run.py "
+                                       f"streams sequences; 'strong': one solve time-sharded over the {world} GPUs)"
+                                       if world > 1 else "single GPU")},
             "cg_iters_per_step": round(float(np.mean(cg_steps)), 2) if cg_steps else None,
-            "cg_iters_per_s": round(float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,
+            "cg_iters_per_s": round(solves * float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,
             "phase_ms": phase_ms,
             "cg_redo": int(st_timed["cg_redo"]),
             "roofline": roof,
@@ -497,8 +568,14 @@ def main():
             "epe": None,
         }
         if roof is not None:
-            roof["step"] = step_roofline(args.cg_mode, world, elapsed / args.steps)
+            roof["step"] = step_roofline(args.cg_mode, world if sharded else 1, elapsed / args.steps)
     s.close()
+    if want_strong:   # (after the headline line exists: the side run's watchdog prints it on a timeout)
+        if line is not None:
+            _PENDING_LINE.append(line)
+        strong = strong_side(args, rdv, rank, world, local_rank, nccl_id, rho0, rhoT)
+        if line is not None:
+            line["strong"] = strong
     if line is not None and world == 1 and args.cg_mode != 0 and not args.no_stencil:
         line["literal_stencil"] = literal_stencil_rate(rho0, rhoT, local_rank)
     # the CPU baselines run after every GPU measurement (no host load beside the timed GPU work),

@@ -115,7 +115,9 @@ typedef struct {
 #define FOTO_K_SPEC      4   /* spectral CG iteration kernel(s)                          */
 #define FOTO_K_DCT       5   /* DCT-II transforms                                        */
 #define FOTO_K_FLOW      6   /* trajectory integration + divergence                      */
-#define FOTO_K_OTHER     7
+#define FOTO_K_SLAB      7   /* sharded: the slab-side x / y DCTs (what the pipelined     */
+                             /* all-to-alls overlap with communication)                  */
+#define FOTO_K_OTHER     FOTO_K_SLAB   /* (older name)                                    */
 
 int foto_bb_opts_default(foto_bb_opts* o);
 int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int Ny, double r,
@@ -203,6 +205,10 @@ int foto_nccl_unique_id(void* out128);
 #define FOTO_XFER_RELAY 3         /* trajectory positions rank j -> j + 1 (flow extraction)   */
 #define FOTO_XFER_DELIVER 4       /* (u, v, m) last rank -> rank 0                            */
 #define FOTO_XFER_HALO2 5         /* two halo planes per side (phi of the fused prox + RHS)   */
+/* the pipelined all-to-alls: arg = part | parts << 8 | halo << 16 (foto_xfer.h
+ * alltoall_part_xfers; the backward one with halo = 1 also delivers phi's halo planes)       */
+#define FOTO_XFER_SLAB_TO_BOX_PART 6
+#define FOTO_XFER_BOX_TO_SLAB_PART 7
 #define FOTO_CALL_SEND 0
 #define FOTO_CALL_RECV 1
 #define FOTO_CALL_COPY 2

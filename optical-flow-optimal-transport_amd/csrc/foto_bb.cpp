@@ -158,6 +158,13 @@ struct foto_bb_ctx {
     bool rccl = false;
     ncclComm_t nc = nullptr;
     hipStream_t s = nullptr;
+    // RCCL: every collective and send / receive group goes on its own stream, ordered against
+    // the compute stream s by events (comm_fork / comm_join), so a group can travel while s
+    // transforms the next part of the slab (the pipelined all-to-alls below)
+    hipStream_t sc = nullptr;
+    hipEvent_t cfork = nullptr, cjoin = nullptr;
+    hipEvent_t cpart[8] = {};      // the backward all-to-all's parts, landed
+    bool phi_halo = false;         // phi's halo planes came with the backward all-to-all
     std::vector<std::unique_ptr<Shard>> sh;   // local shards
     CGScal* hS = nullptr;                     // pinned host mirror of shard 0's CG scalars
     int last_cg = 0;
@@ -209,6 +216,7 @@ struct foto_bb_ctx {
     bool phase_force = false;      // FOTO_PHASE_EV=1: phase events even without kernel timing
     int hpar = 0;                  // slot of the last head
     ~foto_bb_ctx() {
+        if (sc) (void)hipStreamSynchronize(sc);
         if (s) (void)hipStreamSynchronize(s);   // (before the shards free their buffers)
         sh.clear();
         if (nc) (void)ncclCommDestroy(nc);
@@ -218,6 +226,12 @@ struct foto_bb_ctx {
             for (auto e : p) if (e) (void)hipEventDestroy(e);
         for (auto e : fl) if (e) (void)hipEventDestroy(e);
         for (auto e : fin) if (e) (void)hipEventDestroy(e);
+        for (auto e : {cfork, cjoin}) if (e) (void)hipEventDestroy(e);
+        for (auto e : cpart) if (e) (void)hipEventDestroy(e);
+        if (sc) {
+            (void)hipStreamSynchronize(sc);
+            stream_release(sc);
+        }
         if (s) {
             (void)hipStreamSynchronize(s);
             stream_release(s);
@@ -238,14 +252,33 @@ namespace foto {
 // Offsets are in doubles from the pointer a picker returns for the shard (negative: the halo
 // plane below).  The virtual-rank GPU tests therefore run the very lists RCCL executes, and
 // tests/test_xfer.py checks the RCCL call sequences of every rank against each other.
+// compute stream -> communication stream: what s has enqueued so far happens before what sc
+// runs next (RCCL only; virtual ranks run everything on s)
+static int comm_fork(foto_bb_ctx* c) {
+    if (!c->sc) return 0;
+    FOTO_HIP_CHECK(hipEventRecord(c->cfork, c->s));
+    FOTO_HIP_CHECK(hipStreamWaitEvent(c->sc, c->cfork, 0));
+    return 0;
+}
+// communication stream -> compute stream
+static int comm_join(foto_bb_ctx* c) {
+    if (!c->sc) return 0;
+    FOTO_HIP_CHECK(hipEventRecord(c->cjoin, c->sc));
+    FOTO_HIP_CHECK(hipStreamWaitEvent(c->s, c->cjoin, 0));
+    return 0;
+}
+
+// one list, issued on the communication stream (RCCL) or as copies on s (virtual ranks); the
+// caller orders it against s (exchange() below does, the pipelined all-to-alls do per part)
 template <class SrcPick, class DstPick>
-static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, DstPick dp) {
+static int exchange_raw(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, DstPick dp) {
     if (!c->rccl) {
         for (const Xfer& x : xs)
             FOTO_HIP_CHECK(hipMemcpyAsync(dp(*c->sh[x.dst]) + x.doff, sp(*c->sh[x.src]) + x.soff,
                                           (size_t)x.n * sizeof(double), hipMemcpyDeviceToDevice, c->s));
         return 0;
     }
+    hipStream_t st = c->sc ? c->sc : c->s;
     Shard& s = *c->sh[0];
     const std::vector<Call> cs = rccl_calls(xs, s.rank);
     const bool grouped = !cs.empty() && cs.front().op != CALL_COPY;
@@ -257,15 +290,22 @@ static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, Dst
             open = false;
         }
         if (k.op == CALL_SEND)
-            FOTO_NCCL_CHECK(ncclSend(sp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclSend(sp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, st));
         else if (k.op == CALL_RECV)
-            FOTO_NCCL_CHECK(ncclRecv(dp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, c->s));
+            FOTO_NCCL_CHECK(ncclRecv(dp(s) + k.off, (size_t)k.n, ncclDouble, k.peer, c->nc, st));
         else
             FOTO_HIP_CHECK(hipMemcpyAsync(dp(s) + k.doff, sp(s) + k.off, (size_t)k.n * sizeof(double),
-                                          hipMemcpyDeviceToDevice, c->s));
+                                          hipMemcpyDeviceToDevice, st));
     }
     if (open) FOTO_NCCL_CHECK(ncclGroupEnd());
     return 0;
+}
+
+template <class SrcPick, class DstPick>
+static int exchange(foto_bb_ctx* c, const std::vector<Xfer>& xs, SrcPick sp, DstPick dp) {
+    FOTO_TRY(comm_fork(c));
+    FOTO_TRY(exchange_raw(c, xs, sp, dp));
+    return comm_join(c);
 }
 
 // each rank's `cnt` doubles at slot [rank] of the picked array to every rank's same slot
@@ -276,8 +316,9 @@ static int allgather(foto_bb_ctx* c, Pick pick, int cnt) {
     if (c->rccl) {
         Shard& s = *c->sh[0];
         double* base = pick(s);
-        FOTO_NCCL_CHECK(ncclAllGather(base + (size_t)s.rank * cnt, base, cnt, ncclDouble, c->nc, c->s));
-        return 0;
+        FOTO_TRY(comm_fork(c));
+        FOTO_NCCL_CHECK(ncclAllGather(base + (size_t)s.rank * cnt, base, cnt, ncclDouble, c->nc, c->sc ? c->sc : c->s));
+        return comm_join(c);
     }
     return exchange(c, allgather_xfers(c->W, cnt), pick, pick);
 }
@@ -309,6 +350,14 @@ static int ctx_init(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
         ncclUniqueId id;
         memcpy(&id, c->o.nccl_id, sizeof(id));
         FOTO_NCCL_CHECK(ncclCommInitRank(&c->nc, W, id, c->o.rank));
+        // FOTO_COMM_STREAM=0: every RCCL call on the compute stream (A/B runs)
+        const char* cs = getenv("FOTO_COMM_STREAM");
+        if (!(cs && atoi(cs) == 0)) {
+            FOTO_TRY(stream_acquire(&c->sc));
+            FOTO_HIP_CHECK(hipEventCreateWithFlags(&c->cfork, hipEventDisableTiming));
+            FOTO_HIP_CHECK(hipEventCreateWithFlags(&c->cjoin, hipEventDisableTiming));
+            for (auto& e : c->cpart) FOTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
     }
     const int nlocal = c->rccl ? 1 : W;
     {
@@ -439,13 +488,29 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
     return 0;
 }
 
-// all-to-all between the physical slabs and the spectral row boxes (foto_xfer.h)
-static int alltoall_spec(foto_bb_ctx* c, bool forward) {
-    // the slab side is the shard's RHS buffer: fwd_local leaves the x / y DCTs of F there, and
-    // inv_local takes the inverse's slab from it (F is consumed by then)
-    auto sbuf = [&](Shard& s) { return forward ? s.rv : s.spec->box_out(); };
-    auto rbuf = [&](Shard& s) { return forward ? s.spec->box_in() : s.rv; };
-    return exchange(c, alltoall_xfers(c->Nt, c->Ny, c->Nx, c->W, forward), sbuf, rbuf);
+// The slab <-> row-box all-to-alls (foto_xfer.h), pipelined in parts: the forward one sends a
+// part of every slab once its x / y DCTs have run, while the compute stream transforms the next
+// part; the backward one lands in parts and each part's inverse y / x DCTs start as soon as it
+// is in, while the next part travels.  The backward one also delivers phi's halo planes (a2a_halo)
+// -- rows of the neighbours' boundary planes from every box owner, over all links, transformed
+// here with the own planes -- so the fused prox + RHS needs no separate one-plane phi exchange
+// over the single link to each neighbour.  Virtual ranks run the same lists as copies on s.
+// FOTO_A2A_PARTS (default 2, 1..8): parts per direction; FOTO_A2A_HALO=0: phi's halo by the
+// separate exchange (A/B runs).
+static int a2a_parts(const foto_bb_ctx* c) {
+    const char* e = getenv("FOTO_A2A_PARTS");
+    const int v = e ? atoi(e) : 2;
+    return std::max(1, std::min(8, v));
+}
+
+static int a2a_halo(const foto_bb_ctx* c) {
+    if (c->W == 1) return 0;
+    const char* e = getenv("FOTO_A2A_HALO");
+    if (e && atoi(e) == 0) return 0;
+    // the deferred-edge fused prox (and the unfused prox) read one phi halo plane per side; the
+    // edge-recompute variant (FOTO_PR_EDGE=0) reads two and keeps its own exchange
+    const char* pe = getenv("FOTO_PR_EDGE");
+    return (c->fuse && pe && atoi(pe) == 0) ? 0 : 1;
 }
 
 // Spectral CG over time-slab shards, in phases: x/y DCTs on the own planes, all-to-all to row
@@ -456,8 +521,20 @@ static int alltoall_spec(foto_bb_ctx* c, bool forward) {
 // t-DCT, the all-to-all back and the inverse x/y DCTs (sharded_inv).
 static int sharded_fwd(foto_bb_ctx* c) {
     KTimer* kt = &c->kt;
-    for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_local(sp->rv, kt, c->s));
-    FOTO_TRY(alltoall_spec(c, true));
+    const int parts = a2a_parts(c);
+    // the slab side is the shard's RHS buffer: fwd_local leaves the x / y DCTs of F there
+    auto sbuf = [](Shard& s) { return s.rv; };
+    auto rbuf = [](Shard& s) { return s.spec->box_in(); };
+    for (int p = 0; p < parts; ++p) {
+        for (auto& sp : c->sh) {
+            int lo, hi;
+            split_part(sp->g.nloc, parts, p, &lo, &hi);
+            if (hi > lo) FOTO_TRY(sp->spec->fwd_local(sp->rv, lo, hi, kt, c->s));
+        }
+        FOTO_TRY(comm_fork(c));
+        FOTO_TRY(exchange_raw(c, alltoall_part_xfers(c->Nt, c->Ny, c->Nx, c->W, true, p, parts, 0), sbuf, rbuf));
+    }
+    FOTO_TRY(comm_join(c));
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->fwd_t(kt, c->s));
     return 0;
 }
@@ -473,8 +550,24 @@ static int sharded_gauss(foto_bb_ctx* c) {
 static int sharded_inv(foto_bb_ctx* c) {
     KTimer* kt = &c->kt;
     for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_t(kt, c->s));
-    FOTO_TRY(alltoall_spec(c, false));
-    for (auto& sp : c->sh) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, kt, c->s));
+    const int parts = a2a_parts(c), halo = a2a_halo(c);
+    // inv_local takes the inverse's slab (and halo planes) from the RHS buffer (F is consumed by then)
+    auto sbuf = [](Shard& s) { return s.spec->box_out(); };
+    auto rbuf = [](Shard& s) { return s.rv; };
+    FOTO_TRY(comm_fork(c));
+    for (int p = 0; p < parts; ++p) {
+        FOTO_TRY(exchange_raw(c, alltoall_part_xfers(c->Nt, c->Ny, c->Nx, c->W, false, p, parts, halo), sbuf, rbuf));
+        if (c->sc) FOTO_HIP_CHECK(hipEventRecord(c->cpart[p], c->sc));
+    }
+    for (int p = 0; p < parts; ++p) {
+        if (c->sc) FOTO_HIP_CHECK(hipStreamWaitEvent(c->s, c->cpart[p], 0));
+        for (auto& sp : c->sh) {
+            int lo, hi;
+            alltoall_part_planes(c->Nt, c->W, sp->rank, p, parts, halo, &lo, &hi);
+            if (hi > lo) FOTO_TRY(sp->spec->inv_local(sp->rv, sp->phi, lo, hi, kt, c->s));
+        }
+    }
+    c->phi_halo = halo != 0;
     return 0;
 }
 
@@ -618,7 +711,7 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
     const bool defer = W > 1 && !(pe && atoi(pe) == 0);
     if (W > 1) {
         if (defer) {
-            FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+            if (!c->phi_halo) FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
         } else {
             FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
                               [](Shard& s) { return s.phi; }));
@@ -650,6 +743,7 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
                                                s.rb, rr, c->s, gd));
         }
     }
+    c->phi_halo = false;   // (consumed: the next prox's phi comes from the next solve)
     // the stencil CG's F.F (its stopping rule) from every rank
     if (c->o.cg_mode == 0) FOTO_TRY(allgather(c, [](Shard& s) { return s.gath_rr(); }, 1));
     return 0;
@@ -726,7 +820,8 @@ static int outer_tail(foto_bb_ctx* c, size_t kmark) {
             }
         c->f_ready = true;
     } else {
-        FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+        if (!c->phi_halo) FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+        c->phi_halo = false;
         for (auto& sp : c->sh) {
             Shard& s = *sp;
             const double nv = (double)s.g.nloc * (double)s.g.nxy;
@@ -874,7 +969,8 @@ static int outer_complete(foto_bb_ctx* c, double* crit, int* cg_iters, int* cg_i
             if (c->fuse) {
                 FOTO_TRY(prox_rhs(c, false, e.par));
             } else {
-                FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+                if (!c->phi_halo) FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
+                c->phi_halo = false;
                 for (auto& sp : c->sh) {
                     Shard& s = *sp;
                     FOTO_HIP_CHECK(launch_prox(s.g, s.phi, s.mu[0], s.mu[1], s.mu[2], s.q[0], s.q[1], s.q[2], c->r,
@@ -1006,6 +1102,13 @@ int foto_xfer_calls(int kind, int Nt, int Ny, int Nx, int world, int rank, int a
             break;
         case FOTO_XFER_DELIVER: xs = deliver_xfers(nxy, world); break;
         case FOTO_XFER_HALO2: xs = halo_depth_xfers(Nt, nxy, world, 2); break;
+        case FOTO_XFER_SLAB_TO_BOX_PART:
+        case FOTO_XFER_BOX_TO_SLAB_PART: {
+            const int part = arg & 0xff, parts = (arg >> 8) & 0xff, halo = (arg >> 16) & 0xff;
+            if (parts < 1 || part >= parts || halo > 1) { set_error("foto_xfer_calls: bad part / parts / halo"); return FOTO_ERR_ARG; }
+            xs = alltoall_part_xfers(Nt, Ny, Nx, world, kind == FOTO_XFER_SLAB_TO_BOX_PART, part, parts, halo);
+            break;
+        }
         default: set_error("foto_xfer_calls: unknown kind %d", kind); return FOTO_ERR_ARG;
     }
     const std::vector<Call> cs = rccl_calls(xs, rank);

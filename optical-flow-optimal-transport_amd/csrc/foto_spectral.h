@@ -29,14 +29,17 @@ struct SpectralPlan {
     int drop_newest(hipStream_t s);
 
     // ---- sharded phases (driven by foto_bb.cpp, all-to-all / all-gather in between)
-    int fwd_local(double* b, KTimer* kt, hipStream_t s);    // x, y DCT of own planes, in place in b (the all-to-all's source)
+    // x, y DCT of own planes [lo, hi), in place in b (the all-to-all's source)
+    int fwd_local(double* b, int lo, int hi, KTimer* kt, hipStream_t s);
     int fwd_t(KTimer* kt, hipStream_t s);                   // box_in (after all-to-all) -> b^
     int cg_begin(double rtol, int maxiter, KTimer* kt, hipStream_t s);   // r^ = b^, moments -> gath
     int cg_pass(double rtol, int maxiter, KTimer* kt, hipStream_t s);    // planned CG steps, moments -> gath
     int cg_plan(int init, double rtol, int maxiter, hipStream_t s);      // after the all-gather
     int poll(int* done, int* iters, int* passes, hipStream_t s);
     int inv_t(KTimer* kt, hipStream_t s);                   // x^ = (b^ - r^)/lam, inverse t-DCT -> box_out
-    int inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s);   // inverse y, x of scratch (the all-to-all's target) -> x
+    // inverse y, x of planes [lo, hi) of scratch (the all-to-all's target) -> x; lo = -1 / hi =
+    // nloc + 1: the halo plane below / above too (scratch and x halo-padded)
+    int inv_local(double* scratch, double* x, int lo, int hi, KTimer* kt, hipStream_t s);
     double* box_in() const;    // box-side receive buffer [t][rows][x]
     double* box_out() const;   // box-side send buffer of the inverse
     double* gath() const;      // world * moments() doubles

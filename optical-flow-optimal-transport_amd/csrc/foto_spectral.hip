@@ -3150,7 +3150,7 @@ struct SpecImpl {
     int y0 = 0, nyl = 0;          // spectral box rows (sharded: Ny split over ranks)
     double r = 1, eps = 0;
     double *bh = nullptr, *rh = nullptr, *ph = nullptr, *tmp = nullptr;   // spectral box
-    double* tmpp = nullptr;                                                 // physical slab scratch
+    double* tmpp = nullptr;       // physical slab scratch (one halo plane per side: tmpp[-nxy ..])
     double *Cx = nullptr, *Cy = nullptr, *Ct = nullptr, *CxT = nullptr, *CyT = nullptr, *CtT = nullptr;
     double *mx = nullptr, *my = nullptr, *mt = nullptr;
     double *Fx = nullptr, *Fy = nullptr, *Ft = nullptr;   // FFT-DCT tables (nullptr: GEMM path)
@@ -3308,7 +3308,7 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
     FOTO_TRY(P->alloc(NB * 8, &b)); P->ph = (double*)b;
     FOTO_TRY(P->alloc(std::max(NB, NS) * 8, &b)); P->tmp = (double*)b;
     if (world > 1) {
-        FOTO_TRY(P->alloc(NS * 8, &b)); P->tmpp = (double*)b;
+        FOTO_TRY(P->alloc((NS + 2 * (size_t)g.nxy) * 8, &b)); P->tmpp = (double*)b + g.nxy;
     }
     std::vector<double> C, CT, mu;
     if (g_dct_fft < 0) {
@@ -4117,14 +4117,19 @@ int SpectralPlan::solve(double* b, double* x, double rtol, int maxiter, int pred
 // ----------------------------------------------------------------------------- sharded phases
 // Physical slab [tl][y][x] (planes t0..t0+nloc) <-> spectral box [kt][ky - y0][kx].
 
-int SpectralPlan::fwd_local(double* b, KTimer* kt, hipStream_t s) {
+int SpectralPlan::fwd_local(double* b, int lo, int hi, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
+    if (lo < 0 || hi > g.nloc || hi <= lo) {
+        set_error("spectral CG: fwd_local planes [%d, %d) outside the slab", lo, hi);
+        return FOTO_ERR_ARG;
+    }
+    const int np = hi - lo;
+    const int64_t o = (int64_t)lo * g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_pass(P, 0, false, g.nloc * g.Ny, 1, b, P->tmpp, s));      // x
-    FOTO_HIP_CHECK(dct_pass(P, 1, false, g.nloc, g.Nx, P->tmpp, b, s));          // y (b: the all-to-all's source)
-    const int64_t n = (int64_t)g.nloc * g.nxy;
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 4.0 * 8.0 * (double)n);
+    FOTO_HIP_CHECK(dct_pass(P, 0, false, np * g.Ny, 1, b + o, P->tmpp + o, s));   // x
+    FOTO_HIP_CHECK(dct_pass(P, 1, false, np, g.Nx, P->tmpp + o, b + o, s));       // y (b: the all-to-all's source)
+    if (kt) kt->stop(e, s, FOTO_K_SLAB, 4.0 * 8.0 * (double)np * (double)g.nxy);
     return 0;
 }
 
@@ -4195,14 +4200,19 @@ int SpectralPlan::inv_t(KTimer* kt, hipStream_t s) {
     return 0;
 }
 
-int SpectralPlan::inv_local(double* scratch, double* x, KTimer* kt, hipStream_t s) {
+int SpectralPlan::inv_local(double* scratch, double* x, int lo, int hi, KTimer* kt, hipStream_t s) {
     SpecImpl* P = (SpecImpl*)impl;
     const Geo& g = P->g;
-    const int64_t n = (int64_t)g.nloc * g.nxy;
+    if (lo < -1 || hi > g.nloc + 1 || hi <= lo) {   // (one halo plane per side: phi's halo)
+        set_error("spectral CG: inv_local planes [%d, %d) outside the slab and its halo", lo, hi);
+        return FOTO_ERR_ARG;
+    }
+    const int np = hi - lo;
+    const int64_t o = (int64_t)lo * g.nxy;
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    FOTO_HIP_CHECK(dct_pass(P, 1, true, g.nloc, g.Nx, scratch, P->tmpp, s));     // y (scratch: the all-to-all's target)
-    FOTO_HIP_CHECK(dct_pass(P, 0, true, g.nloc * g.Ny, 1, P->tmpp, x, s));       // x
-    if (kt) kt->stop(e, s, FOTO_K_DCT, 4.0 * 8.0 * (double)n);
+    FOTO_HIP_CHECK(dct_pass(P, 1, true, np, g.Nx, scratch + o, P->tmpp + o, s));   // y (scratch: the all-to-all's target)
+    FOTO_HIP_CHECK(dct_pass(P, 0, true, np * g.Ny, 1, P->tmpp + o, x + o, s));     // x
+    if (kt) kt->stop(e, s, FOTO_K_SLAB, 4.0 * 8.0 * (double)np * (double)g.nxy);
     return 0;
 }
 

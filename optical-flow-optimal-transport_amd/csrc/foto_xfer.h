@@ -94,6 +94,64 @@ inline std::vector<Xfer> alltoall_xfers(int Nt, int Ny, int Nx, int W, bool forw
     return xs;
 }
 
+// part `part` of `parts` of n items: [part n / parts, (part + 1) n / parts)
+inline void split_part(int n, int parts, int part, int* lo, int* hi) {
+    *lo = (int)((int64_t)part * n / parts);
+    *hi = (int)((int64_t)(part + 1) * n / parts);
+}
+
+// The pipelined all-to-alls (foto_bb.cpp sharded_fwd / sharded_inv): the same transfers as
+// alltoall_xfers, issued in `parts` groups so a group travels on the communication stream while
+// the compute stream transforms the next one.
+//   forward, part p: the planes of part p of every SOURCE slab (sent once their x / y DCTs ran);
+//   backward, part p: the planes of part p of every DESTINATION slab (transformed back once they
+//   arrived), with `halo` (0 or 1) extra planes per side -- the lower halo plane (t0 - 1) with
+//   the first part, the upper one (t0 + nloc) with the last, landing in the slab's halo planes
+//   (local -1, nloc); planes outside [0, Nt) are not sent.  The inverse x / y DCTs then run on
+//   nloc + 2 planes and phi arrives with the halo plane the fused prox + RHS reads: rows of it
+//   from every box owner, over all links, instead of a whole plane from one neighbour over one.
+// parts = 1, halo = 0: alltoall_xfers' lists, in the same order.
+inline std::vector<Xfer> alltoall_part_xfers(int Nt, int Ny, int Nx, int W, bool forward, int part, int parts,
+                                             int halo) {
+    std::vector<Xfer> xs;
+    const int64_t nxy = (int64_t)Nx * Ny;
+    for (int a = 0; a < W; ++a)
+        for (int b = 0; b < W; ++b) {
+            int ta, na, tb, nb, ya, nya, yb, nyb;
+            split_planes(Nt, W, a, &ta, &na);
+            split_planes(Nt, W, b, &tb, &nb);
+            split_planes(Ny, W, a, &ya, &nya);
+            split_planes(Ny, W, b, &yb, &nyb);
+            if (forward) {
+                int lo, hi;
+                split_part(na, parts, part, &lo, &hi);
+                for (int tl = lo; tl < hi; ++tl)
+                    if (nyb > 0)
+                        xs.push_back({a, b, tl * nxy + (int64_t)yb * Nx, (int64_t)(ta + tl) * nyb * Nx,
+                                      (int64_t)nyb * Nx});
+            } else {
+                int lo, hi;
+                split_part(nb, parts, part, &lo, &hi);
+                if (halo && part == 0 && tb > 0) lo -= 1;
+                if (halo && part == parts - 1 && tb + nb < Nt) hi += 1;
+                for (int tl = lo; tl < hi; ++tl)
+                    if (nya > 0)
+                        xs.push_back({a, b, (int64_t)(tb + tl) * nya * Nx, tl * nxy + (int64_t)ya * Nx,
+                                      (int64_t)nya * Nx});
+            }
+        }
+    return xs;
+}
+
+// the local planes [lo, hi) a backward part delivers to rank g (halo planes included)
+inline void alltoall_part_planes(int Nt, int W, int g, int part, int parts, int halo, int* lo, int* hi) {
+    int t0, nl;
+    split_planes(Nt, W, g, &t0, &nl);
+    split_part(nl, parts, part, lo, hi);
+    if (halo && part == 0 && t0 > 0) *lo -= 1;
+    if (halo && part == parts - 1 && t0 + nl < Nt) *hi += 1;
+}
+
 // trajectory positions after rank j's planes -> rank j + 1 (one list per field, px and py)
 inline std::vector<Xfer> relay_xfers(int64_t nxy, int j) { return {{j, j + 1, 0, 0, nxy}}; }
 

@@ -18,8 +18,11 @@ FOTO_ERR_COMM = -3
 FOTO_ERR_STATE = -4
 FOTO_ERR_BC = -5
 
-K_CG_DIR, K_CG_UPD, K_RHS, K_PROX, K_SPEC, K_DCT, K_FLOW, K_OTHER = range(8)
-K_NAMES = ["cg_dir", "cg_upd", "rhs", "prox", "spec_cg", "dct", "flow", "other"]
+K_CG_DIR, K_CG_UPD, K_RHS, K_PROX, K_SPEC, K_DCT, K_FLOW, K_SLAB = range(8)
+K_OTHER = K_SLAB
+# dct_slab: the sharded path's slab-side x / y DCTs (foto.h FOTO_K_SLAB), apart from "dct" (the
+# box-side t axis, x^) so the scaling proxy sees what the pipelined all-to-alls overlap
+K_NAMES = ["cg_dir", "cg_upd", "rhs", "prox", "spec_cg", "dct", "flow", "dct_slab"]
 
 
 class FotoError(RuntimeError):

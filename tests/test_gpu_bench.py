@@ -42,3 +42,33 @@ def test_bench_json_line():
     st = r["step"]
     assert st["alg_bytes_per_voxel"] == sum(st["items"].values()) == 188
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None
+
+
+def test_bench_two_ranks_batch_mode_one_gpu(tmp_path):
+    """bench.py --gpus 2 as the driver launches it (torch.distributed.run, one process per rank,
+    the file rendezvous), both ranks on this one GPU (FOTO_BENCH_DEVICES=0,0): the default batch
+    mode -- one 640x480x32 solve per rank, value = both solves' outer iterations per second on the
+    slowest rank's clock, "scaling": "weak".  (The time-sharded side run needs two GPUs for RCCL:
+    --no-strong here; its call sequences are checked by tests/test_gpu_rccl_mock.py.)"""
+    # (the two ranks started here the way torch.distributed.run starts them -- children of one
+    # process, RANK / WORLD_SIZE / LOCAL_RANK / MASTER_PORT set -- without its torch import)
+    procs = []
+    for g in range(2):
+        env = dict(os.environ, FOTO_BENCH_DEVICES="0,0", WORLD_SIZE="2", RANK=str(g), LOCAL_RANK=str(g),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT="29617")
+        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline", "--no-gn", "--no-stencil", "--no-strong"]
+        procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [ln for o, _ in outs for ln in o.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, [o[-1000:] for o, _ in outs]   # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 3
+    assert "data-parallel x2" in d["config"]["parallelism"]
+    # two problems advanced in the timed region: value = 2 K / elapsed
+    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 2.0) < 0.02
+    assert 150 <= d["cg_iters_per_step"] <= 210
+    assert "strong" not in d

@@ -157,3 +157,37 @@ def test_rccl_path_c4_w8():
     assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
     np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)
     assert all(r["redo"] == 0 for r in ranks)
+
+
+@pytest.mark.parametrize("W", [2, 3, 5])
+def test_rccl_comm_stream_pipelined_alltoall_and_phi_halo(monkeypatch, W):
+    """The communication stream and the pipelined all-to-alls (foto_bb.cpp comm_fork / comm_join,
+    sharded_fwd / sharded_inv: 1, 2 or 3 parts per direction; phi's halo planes delivered by the
+    backward all-to-all, FOTO_A2A_HALO) change only where and when data travels: every variant,
+    over the mock RCCL and as virtual ranks, equals the plain sequence (one part, the separate
+    phi halo exchange, every call on the compute stream) bit for bit.  Nt = 7: slabs of one to
+    four planes, so some ranks have empty parts; the textured pair gives the flow something to
+    carry."""
+    from foto.synthetic import textured_pair
+    Nt, Nx, Ny = 7, 48, 40
+    rho0, rhoT = textured_pair(Nx, Ny, seed=5, dx=1.0, dy=0.5)
+    L = _mock()
+    for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("FOTO_A2A_PARTS", "1")
+    monkeypatch.setenv("FOTO_A2A_HALO", "0")
+    monkeypatch.setenv("FOTO_COMM_STREAM", "0")
+    plain = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    for env in ({}, {"FOTO_A2A_PARTS": "3"}, {"FOTO_A2A_HALO": "0"}, {"FOTO_COMM_STREAM": "0"}):
+        for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+        virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+        compare(ranks, virt, Nt, Nx, Ny, W)
+        for a, b in zip(ranks, plain):
+            assert a["crit"] == b["crit"] and a["cg"] == b["cg"], env
+            np.testing.assert_array_equal(a["phi"], b["phi"])
+        for a, b in zip(ranks[0]["flow"], plain[0]["flow"]):
+            np.testing.assert_array_equal(a, b)

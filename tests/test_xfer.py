@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 XFER_HALO, XFER_SLAB_TO_BOX, XFER_BOX_TO_SLAB, XFER_RELAY, XFER_DELIVER, XFER_HALO2 = range(6)
+XFER_SLAB_TO_BOX_PART, XFER_BOX_TO_SLAB_PART = 6, 7
 SEND, RECV, COPY = range(3)
 
 GRIDS = [(32, 480, 640), (32, 388, 584), (64, 1024, 1024)]   # (Nt, Ny, Nx)
@@ -53,9 +54,9 @@ def src_extent(kind, Nt, Ny, Nx, W, g):
         return -nxy, (nl + 1) * nxy
     if kind == XFER_HALO2:
         return 0, nl * nxy                      # own planes only (halos come from their owners)
-    if kind == XFER_SLAB_TO_BOX:
+    if kind in (XFER_SLAB_TO_BOX, XFER_SLAB_TO_BOX_PART):
         return 0, nl * nxy                      # the slab [tl][y][x] (the rank's RHS buffer)
-    if kind == XFER_BOX_TO_SLAB:
+    if kind in (XFER_BOX_TO_SLAB, XFER_BOX_TO_SLAB_PART):
         return 0, Nt * nyl * Nx                 # box_out: [t][own rows][x]
     return 0, nxy                               # px / py / fu, fv, fm
 
@@ -68,10 +69,12 @@ def dst_extent(kind, Nt, Ny, Nx, W, g):
         return -nxy, (nl + 1) * nxy
     if kind == XFER_HALO2:
         return -2 * nxy, (nl + 2) * nxy
-    if kind == XFER_SLAB_TO_BOX:
+    if kind in (XFER_SLAB_TO_BOX, XFER_SLAB_TO_BOX_PART):
         return 0, max(Nt * nyl * Nx, nl * nxy)   # box_in (the spectral tmp buffer)
     if kind == XFER_BOX_TO_SLAB:
         return 0, nl * nxy                       # the slab [tl][y][x]
+    if kind == XFER_BOX_TO_SLAB_PART:
+        return -nxy, (nl + 1) * nxy              # the slab with one halo plane per side
     return 0, nxy
 
 
@@ -260,3 +263,83 @@ def test_bad_arguments_rejected():
     assert L.foto_xfer_calls(9, 8, 8, 8, 2, 0, 0, out, 1, ctypes.byref(cnt)) == _lib.FOTO_ERR_ARG          # kind
     assert L.foto_xfer_calls(XFER_RELAY, 8, 8, 8, 2, 0, 1, out, 1, ctypes.byref(cnt)) == _lib.FOTO_ERR_ARG  # step
     assert L.foto_xfer_calls(XFER_SLAB_TO_BOX, 8, 8, 8, 4, 0, 0, out, 1, ctypes.byref(cnt)) == _lib.FOTO_ERR_ARG  # cap
+
+
+def part_arg(part, parts, halo=0):
+    return part | (parts << 8) | (halo << 16)
+
+
+def part_planes(Nt, W, g, part, parts, halo):
+    """foto_xfer.h alltoall_part_planes: the local planes a backward part delivers to rank g."""
+    t0, nl = split(Nt, W, g)
+    lo, hi = part * nl // parts, (part + 1) * nl // parts
+    if halo and part == 0 and t0 > 0:
+        lo -= 1
+    if halo and part == parts - 1 and t0 + nl < Nt:
+        hi += 1
+    return lo, hi
+
+
+@pytest.mark.parametrize("grid", GRIDS, ids=lambda g: "x".join(map(str, g[::-1])))
+@pytest.mark.parametrize("W", [2, 3, 5, 8])
+def test_pipelined_alltoall_parts_pair_and_cover(grid, W):
+    """The pipelined all-to-alls (foto_bb.cpp sharded_fwd / sharded_inv): every part pairs on its
+    own (each part is one RCCL group), the forward parts together are the plain forward list,
+    and the backward parts deliver exactly the planes alltoall_part_planes says -- the own
+    planes tiled once, plus phi's halo planes (t0 - 1, t0 + nloc where they exist) with halo = 1."""
+    Nt, Ny, Nx = grid
+    nxy = Nx * Ny
+    full_fwd = [sorted(c) for c in all_calls(XFER_SLAB_TO_BOX, Nt, Ny, Nx, W)]
+    full_bwd = [sorted(c) for c in all_calls(XFER_BOX_TO_SLAB, Nt, Ny, Nx, W)]
+    for parts in (1, 2, 3):
+        got_fwd = [[] for _ in range(W)]
+        for halo in (0, 1):
+            got_bwd = [[] for _ in range(W)]
+            for part in range(parts):
+                cf = all_calls(XFER_SLAB_TO_BOX_PART, Nt, Ny, Nx, W, part_arg(part, parts))
+                check_pairing(cf, W)
+                check_bounds_and_tiling(XFER_SLAB_TO_BOX_PART, cf, Nt, Ny, Nx, W, None)
+                if halo == 0:
+                    for g in range(W):
+                        got_fwd[g] += cf[g]
+                cb = all_calls(XFER_BOX_TO_SLAB_PART, Nt, Ny, Nx, W, part_arg(part, parts, halo))
+                check_pairing(cb, W)
+                check_bounds_and_tiling(XFER_BOX_TO_SLAB_PART, cb, Nt, Ny, Nx, W, None)
+                for g in range(W):
+                    got_bwd[g] += cb[g]
+                    lo, hi = part_planes(Nt, W, g, part, parts, halo)
+                    landed = sorted({(c[2] if c[0] == RECV else c[4]) // nxy for c in cb[g] if c[0] in (RECV, COPY)})
+                    assert landed == list(range(lo, hi)), (parts, part, halo, g, landed, lo, hi)
+            for g in range(W):
+                if halo == 0:
+                    assert sorted(got_bwd[g]) == full_bwd[g]
+        for g in range(W):
+            assert sorted(got_fwd[g]) == full_fwd[g]
+
+
+@pytest.mark.parametrize("W", [2, 3, 5])
+def test_replayed_backward_alltoall_delivers_phi_halo(W):
+    """Replaying the backward parts with halo = 1 on numpy buffers: every rank's slab planes and
+    its two halo planes (where they exist) hold the right rows of the global volume, planes
+    outside [0, Nt) stay untouched."""
+    Nt, Ny, Nx = 9, 7, 5
+    rng = np.random.default_rng(W)
+    G = rng.standard_normal((Nt, Ny, Nx))
+    nxy = Nx * Ny
+    slabs = [split(Nt, W, g) for g in range(W)]
+    boxes = [split(Ny, W, g) for g in range(W)]
+    box_out = {g: (G[:, y0:y0 + nyl, :].ravel().copy(), 0) for g, (y0, nyl) in enumerate(boxes)}
+    dst = {g: (np.full((nl + 2) * nxy, np.nan), nxy) for g, (t0, nl) in enumerate(slabs)}
+    for parts in (2, 3):
+        for g in dst:
+            dst[g][0][:] = np.nan
+        for part in range(parts):
+            replay(XFER_BOX_TO_SLAB_PART, Nt, Ny, Nx, W, box_out, dst, part_arg(part, parts, 1))
+        for g, (t0, nl) in enumerate(slabs):
+            f = dst[g][0].reshape(nl + 2, Ny, Nx)
+            for h in range(-1, nl + 1):
+                if 0 <= t0 + h < Nt:
+                    np.testing.assert_array_equal(f[h + 1], G[t0 + h])
+                else:
+                    assert np.all(np.isnan(f[h + 1]))
+

@@ -11,12 +11,18 @@ moment all-gathers, the slab <-> row-box all-to-alls, RCCL launch latency) is EX
 the curve is an upper bound on what W GPUs can reach.
 
 A communication MODEL is printed beside it (not a measurement: the RCCL calls have only run
-through the in-process transport): per rank and outer iteration the slab <-> row-box
-all-to-alls (each rank sends (W-1)/W of its slab each way, one peer per xGMI link), the
-one-plane phi and w_t halos of the fused prox + RHS with deferred slab edges (both
-neighbours; FOTO_PR_EDGE=0's recompute would send 2 phi + 3 mu planes), the 32-KB
-histogram all-gather and the crit all-gather, at LINK_GBS per direction per link and
-LAT_US per RCCL call.
+through the in-process transport).  Per rank and outer iteration (round 5 structure,
+foto_bb.cpp sharded_fwd / sharded_inv / prox_rhs):
+  * the slab -> box all-to-all, (W-1)/W of the rank's slab, one peer per xGMI link over
+    min(W-1, 7) links, in PARTS groups on the communication stream, each sent while the compute
+    stream runs the next part's x / y DCTs (dct_slab, measured per rank): a two-stage pipeline
+    of PARTS equal parts takes C/P + (P-1) max(C, M)/P + M/P for compute C and transfer M;
+  * the box -> slab all-to-all likewise, carrying phi's halo planes (one per side) as well, so
+    the inverse x / y DCTs run on nloc + 2 planes (their extra compute is added);
+  * the w_t halo of the deferred slab edges: one plane with each neighbour (both at once);
+  * the 32-KB histogram all-gather and the crit all-gather;
+at LINK_GBS per direction per link and LAT_US per RCCL call.  --no-overlap prints round 4's
+model (phi halo a separate plane per neighbour, nothing overlapped) for comparison.
 
     python tools/proxy_scaling.py [--grid 640,480,32 | c4] [--worlds 1,2,4,8] [--steps 10] [--warmup 3] [--out FILE]
 """
@@ -37,18 +43,36 @@ LINK_GBS = 64.0   # xGMI, effective GB/s per direction of one link (7 links x ~1
 LAT_US = 10.0     # per RCCL call (grouped send / recv or all-gather) at these message sizes
 
 
-def comm_model_us(W):
-    """Modelled communication per rank per outer iteration (see the docstring)."""
+PARTS = 2         # FOTO_A2A_PARTS default (foto_bb.cpp a2a_parts)
+
+
+def pipe_us(c_us, m_us, parts):
+    """A two-stage pipeline (compute then transfer, or transfer then compute) of `parts` equal
+    parts: the time beyond the compute alone."""
+    p = max(1, parts)
+    return c_us / p + (p - 1) * max(c_us, m_us) / p + m_us / p - c_us
+
+
+def comm_model_us(W, slab_ms=0.0, overlap=True):
+    """Modelled communication time per rank per outer iteration that the compute does not hide
+    (see the docstring).  slab_ms: the rank's measured slab-side x / y DCT time (both directions)."""
     if W == 1:
         return 0.0, {}
     nl = -(-NT // W)                          # the largest slab
     plane = NX * NY * 8
-    a2a = nl * plane * (W - 1) / W            # bytes one rank sends in one all-to-all
-    # W - 1 peers over 7 links (8 GPUs fully connected): a2a spread over min(W - 1, 7) links
-    a2a_us = a2a / min(W - 1, 7) / (LINK_GBS * 1e3) + LAT_US
-    halo_us = 2 * plane / (LINK_GBS * 1e3) + 2 * LAT_US       # per neighbour: phi, then w_t, one plane each
-    gath_us = 2 * LAT_US                                      # histogram (32 KB) + crit all-gathers
-    parts = {"alltoall_x2": 2 * a2a_us, "halos": halo_us, "allgathers": gath_us}
+    links = min(W - 1, 7)
+    bw = LINK_GBS * 1e3                       # bytes per us
+    a2a = nl * plane * (W - 1) / W / links / bw
+    if not overlap:                           # round 4: no overlap, phi halo its own plane
+        parts = {"alltoall_x2": 2 * (a2a + LAT_US), "halos": 2 * (plane / bw + LAT_US), "allgathers": 2 * LAT_US}
+        return sum(parts.values()), parts
+    c = 1e3 * slab_ms / 2                     # x / y DCTs of one direction
+    a2a_i = (nl + 2) * plane * (W - 1) / W / links / bw   # + phi's two halo planes
+    parts = {"alltoall_fwd": pipe_us(c, a2a, PARTS) + PARTS * LAT_US,
+             "alltoall_inv": pipe_us(c, a2a_i, PARTS) + PARTS * LAT_US,
+             "halo_dct": c * 2 / nl,          # the inverse x / y DCTs of the two halo planes
+             "halo_wt": plane / bw + LAT_US,
+             "allgathers": 2 * LAT_US}
     return sum(parts.values()), parts
 
 
@@ -83,6 +107,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-overlap", action="store_true", help="round 4's communication model")
     args = ap.parse_args()
     global NX, NY, NT
     NX, NY, NT = (1024, 1024, 64) if args.grid == "c4" else (int(v) for v in args.grid.split(","))
@@ -97,16 +122,22 @@ def main():
     for r in rows:
         k = r["kernels_ms"]
         eff = base / (r["W"] * r["rank_ms"])
-        cm, parts = comm_model_us(r["W"])
+        cm, parts = comm_model_us(r["W"], k.get("dct_slab", 0.0), overlap=not args.no_overlap)
         r["comm_model_us"] = {"total": cm, **parts}
         model_ms = r["rank_ms"] + cm / 1e3
         lines.append(f"  {r['W']:>2} {r['rank_ms']:10.3f} {1e3 / r['rank_ms']:10.1f} {eff:5.2f} {r['cg_its']:6.1f} "
-                     f"{r['launches'].get('spec_cg', 0):13.1f} {k.get('spec_cg', 0):8.3f} {k.get('dct', 0):7.3f} "
-                     f"{k.get('prox', 0) + k.get('rhs', 0):11.3f} {k.get('flow', 0) + k.get('other', 0):10.3f} "
+                     f"{r['launches'].get('spec_cg', 0):13.1f} {k.get('spec_cg', 0):8.3f} {k.get('dct', 0) + k.get('dct_slab', 0):7.3f} "
+                     f"{k.get('prox', 0) + k.get('rhs', 0):11.3f} {k.get('flow', 0):10.3f} "
                      f"{cm / 1e3:13.3f} {1e3 / model_ms:10.1f} {base / (r['W'] * model_ms):9.2f}")
-    lines.append(f"# comm model: all-to-all bytes (W-1)/W of the rank's slab each way over min(W-1, 7) xGMI links, "
-                 f"halos 2 planes per neighbour (phi, w_t), {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
-                 f"(a model, not a measurement; no overlap with compute assumed).")
+    if args.no_overlap:
+        lines.append(f"# comm model (round 4): all-to-all bytes (W-1)/W of the rank's slab each way over min(W-1, 7) xGMI "
+                     f"links, halos 2 planes per neighbour (phi, w_t), {LINK_GBS:.0f} GB/s per link direction, "
+                     f"{LAT_US:.0f} us per RCCL call, no overlap (a model, not a measurement).")
+    else:
+        lines.append(f"# comm model (round 5): the all-to-alls pipelined in {PARTS} parts against the slab-side x / y DCTs "
+                     f"(dct_slab, measured), phi's halo planes inside the backward all-to-all (+2 planes of inverse DCT), "
+                     f"w_t one plane per neighbour, {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
+                     f"(a model, not a measurement).")
     lines.append("# cg: the CG kernels as timed by the library (mode 3: the Gauss-compressed CG's histogram and "
                  "node solve groups; mode 2: the s-step passes, incl. a deferred solve's no-op margin passes).")
     lines.append("# rank ms/it = what one rank's GPU computes per outer iteration; one_device_wall_ms in the JSON below is")
