@@ -495,18 +495,24 @@ static int cg_iteration(foto_bb_ctx* c, int k) {
 // -- rows of the neighbours' boundary planes from every box owner, over all links, transformed
 // here with the own planes -- so the fused prox + RHS needs no separate one-plane phi exchange
 // over the single link to each neighbour.  Virtual ranks run the same lists as copies on s.
-// FOTO_A2A_PARTS (default 2, 1..8): parts per direction; FOTO_A2A_HALO=0: phi's halo by the
-// separate exchange (A/B runs).
+// Both pay off where a plane is large against the compute it adds (two planes of inverse x / y
+// DCT for the halo, twice the DCT launches for two parts): by default they are on for planes of
+// >= 2^19 voxels (C4's 1024 x 1024: 8.4 MB per plane, 131 us over one link; 2 parts, the halo
+// inside) and off below (the bench grid's 640 x 480: 2.5 MB, where the compute-only proxy gave
+// 0.337 against 0.300 ms per rank at W = 8 with them on, profiles/r05_proxy_scaling.txt).
+// FOTO_A2A_PARTS (1..8) and FOTO_A2A_HALO (0 / 1) override (A/B runs, tests).
+static bool a2a_big_planes(const foto_bb_ctx* c) { return (int64_t)c->Nx * c->Ny >= (1 << 19); }
+
 static int a2a_parts(const foto_bb_ctx* c) {
     const char* e = getenv("FOTO_A2A_PARTS");
-    const int v = e ? atoi(e) : 2;
+    const int v = e ? atoi(e) : (a2a_big_planes(c) ? 2 : 1);
     return std::max(1, std::min(8, v));
 }
 
 static int a2a_halo(const foto_bb_ctx* c) {
     if (c->W == 1) return 0;
     const char* e = getenv("FOTO_A2A_HALO");
-    if (e && atoi(e) == 0) return 0;
+    if (e ? atoi(e) == 0 : !a2a_big_planes(c)) return 0;
     // the deferred-edge fused prox (and the unfused prox) read one phi halo plane per side; the
     // edge-recompute variant (FOTO_PR_EDGE=0) reads two and keeps its own exchange
     const char* pe = getenv("FOTO_PR_EDGE");

@@ -43,7 +43,14 @@ LINK_GBS = 64.0   # xGMI, effective GB/s per direction of one link (7 links x ~1
 LAT_US = 10.0     # per RCCL call (grouped send / recv or all-gather) at these message sizes
 
 
-PARTS = 2         # FOTO_A2A_PARTS default (foto_bb.cpp a2a_parts)
+def a2a_setup():
+    """foto_bb.cpp a2a_parts / a2a_halo defaults (and their environment overrides): two parts and
+    phi's halo inside the backward all-to-all for planes of >= 2^19 voxels, else one part and the
+    separate halo plane."""
+    big = NX * NY >= (1 << 19)
+    parts = int(os.environ.get("FOTO_A2A_PARTS", "2" if big else "1"))
+    halo = int(os.environ.get("FOTO_A2A_HALO", "1" if big else "0"))
+    return max(1, min(8, parts)), halo
 
 
 def pipe_us(c_us, m_us, parts):
@@ -66,11 +73,13 @@ def comm_model_us(W, slab_ms=0.0, overlap=True):
     if not overlap:                           # round 4: no overlap, phi halo its own plane
         parts = {"alltoall_x2": 2 * (a2a + LAT_US), "halos": 2 * (plane / bw + LAT_US), "allgathers": 2 * LAT_US}
         return sum(parts.values()), parts
-    c = 1e3 * slab_ms / 2                     # x / y DCTs of one direction
-    a2a_i = (nl + 2) * plane * (W - 1) / W / links / bw   # + phi's two halo planes
-    parts = {"alltoall_fwd": pipe_us(c, a2a, PARTS) + PARTS * LAT_US,
-             "alltoall_inv": pipe_us(c, a2a_i, PARTS) + PARTS * LAT_US,
-             "halo_dct": c * 2 / nl,          # the inverse x / y DCTs of the two halo planes
+    P, halo = a2a_setup()
+    c = 1e3 * slab_ms / 2                     # x / y DCTs of one direction (measured: incl. the halo
+    #                                           planes' inverse DCTs when they are delivered)
+    a2a_i = (nl + 2 * halo) * plane * (W - 1) / W / links / bw   # + phi's two halo planes
+    parts = {"alltoall_fwd": pipe_us(c, a2a, P) + P * LAT_US,
+             "alltoall_inv": pipe_us(c, a2a_i, P) + P * LAT_US,
+             "halo_phi": 0.0 if halo else plane / bw + LAT_US,
              "halo_wt": plane / bw + LAT_US,
              "allgathers": 2 * LAT_US}
     return sum(parts.values()), parts
@@ -134,8 +143,10 @@ def main():
                      f"links, halos 2 planes per neighbour (phi, w_t), {LINK_GBS:.0f} GB/s per link direction, "
                      f"{LAT_US:.0f} us per RCCL call, no overlap (a model, not a measurement).")
     else:
-        lines.append(f"# comm model (round 5): the all-to-alls pipelined in {PARTS} parts against the slab-side x / y DCTs "
-                     f"(dct_slab, measured), phi's halo planes inside the backward all-to-all (+2 planes of inverse DCT), "
+        P, halo = a2a_setup()
+        lines.append(f"# comm model (round 5): the all-to-alls in {P} part(s) on the communication stream, pipelined "
+                     f"against the slab-side x / y DCTs (dct_slab, measured), phi's halo planes "
+                     f"{'inside the backward all-to-all (their inverse DCT is in the measured compute)' if halo else 'as one plane per neighbour'}, "
                      f"w_t one plane per neighbour, {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
                      f"(a model, not a measurement).")
     lines.append("# cg: the CG kernels as timed by the library (mode 3: the Gauss-compressed CG's histogram and "
