@@ -754,19 +754,28 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #ifndef FOTO_PR_X
 #define FOTO_PR_X 64
 #endif
-constexpr int PR_X = FOTO_PR_X, PR_Y = FOTO_PR_Y, PR_NT = PR_X * PR_Y;   // 512 threads (64 x 8)
+// own voxels per thread (FOTO_PR_VPT=2 with FOTO_PR_Y=16: a 64 x 16 tile on 512 threads, rows y and
+// y + 8 per thread, the ring 164 voxels for 1024 instead of 148 for 512; 81.5 KB of LDS, so one
+// block per CU at up to 256 VGPRs)
+#ifndef FOTO_PR_VPT
+#define FOTO_PR_VPT 1
+#endif
+constexpr int PR_X = FOTO_PR_X, PR_Y = FOTO_PR_Y, PR_VPT = FOTO_PR_VPT;
+constexpr int PR_NT = PR_X * PR_Y / PR_VPT;                 // 512 threads (64 x 8)
+constexpr int PR_YV = PR_Y / PR_VPT;                        // rows between a thread's own voxels
 constexpr int PR_PW = PR_X + 2, PR_PH = PR_Y + 2;         // stepB region
 constexpr int PR_FW = PR_X + 4, PR_FH = PR_Y + 4;         // phi region
 constexpr int PR_HALO = 2 * PR_PW + 2 * PR_Y;             // 148 ring voxels (64 x 8)
 constexpr int PR_FN = PR_FW * PR_FH;                      // 816 phi values per plane
 constexpr int PR_FR = (PR_FN + PR_NT - 1) / PR_NT;        // phi loads per thread per plane
-static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT,   // (32 x 16, 16 x 32, 32 x 8: slower, r03)
-              "one voxel per thread, ring voxels on the first threads");
+static_assert(PR_X == 64 && PR_NT <= 1024 && PR_HALO <= PR_NT && PR_Y % PR_VPT == 0,   // (32 x 16, 16 x 32, 32 x 8: slower, r03)
+              "whole rows per thread, ring voxels on the first threads");
+constexpr int PR_WPE = PR_VPT == 1 ? 4 : 2;               // waves per SIMD (VGPR budget 128 / 256)
 
 // EDGE: the deferred-edge variant (sharded); the single-shard instantiation carries none of its
 // code (its extra registers spilled the kernel at the 128-VGPR cap: 171 -> 184 us)
 template <bool EDGE>
-__global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_prox_rhs(
+__global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(PR_WPE))) void k_prox_rhs(
         Geo g, const double* __restrict__ phi, const double* __restrict__ mut, const double* __restrict__ mux,
         const double* __restrict__ muy, double* __restrict__ nut, double* __restrict__ nux, double* __restrict__ nuy,
         const double* __restrict__ rho0, const double* __restrict__ rhoT, double r, double inv_r,
@@ -783,12 +792,19 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     const int l0 = ch * tch, l1 = min(g.nloc, l0 + tch);   // own planes of this chunk (local)
     const int x0 = (tile % ntx) * PR_X, y0 = (tile / ntx) * PR_Y;
     const int tid = threadIdx.x;
-    // own voxel: stepB region position (1 + tid % 64, 1 + tid / 64)
-    const int opx = 1 + (tid & (PR_X - 1)), opy = 1 + tid / PR_X;
-    const int ox = x0 - 1 + opx, oy = y0 - 1 + opy;
-    const bool own = ox < Nx && oy < Ny;
-    const int ooff = own ? oy * Nx + ox : 0;   // in-plane offsets fit 32 bits
-    // ring voxel of threads 0..147
+    // own voxels: stepB region positions (1 + tid % 64, 1 + tid / 64 + v PR_YV)
+    const int opx = 1 + (tid & (PR_X - 1));
+    const int ox = x0 - 1 + opx;
+    int opy[PR_VPT], oy[PR_VPT], ooff[PR_VPT];
+    bool own[PR_VPT];
+#pragma unroll
+    for (int v = 0; v < PR_VPT; ++v) {
+        opy[v] = 1 + tid / PR_X + v * PR_YV;
+        oy[v] = y0 - 1 + opy[v];
+        own[v] = ox < Nx && oy[v] < Ny;
+        ooff[v] = own[v] ? oy[v] * Nx + ox : 0;   // in-plane offsets fit 32 bits
+    }
+    // ring voxel of threads 0..PR_HALO-1
     int hpx = 0, hpy = 0;
     if (tid < PR_PW) { hpx = tid; hpy = 0; }
     else if (tid < 2 * PR_PW) { hpx = tid - PR_PW; hpy = PR_PH - 1; }
@@ -831,19 +847,24 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     };
     auto load_phi = [&](int p) { load_phi_to(p, fv); };
     auto store_phi = [&](int p) { store_phi_from(p, fv); };
-    // mu of the own and the ring voxel, one plane ahead
-    double om[3] = {0.0, 0.0, 0.0}, hm[3] = {0.0, 0.0, 0.0};
+    // mu of the own and the ring voxels, one plane ahead
+    double om[PR_VPT][3], hm[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int v = 0; v < PR_VPT; ++v) om[v][0] = om[v][1] = om[v][2] = 0.0;
     auto load_mu = [&](int p) {
         if (p > pz) return;
+#pragma unroll
+        for (int v = 0; v < PR_VPT; ++v) {
 #if FOTO_PR_NTLD
-        if (own) {   // (the old mu is dead after this kernel; ring voxels keep plain loads)
-            om[0] = __builtin_nontemporal_load(&mut[p * nxy + ooff]);
-            om[1] = __builtin_nontemporal_load(&mux[p * nxy + ooff]);
-            om[2] = __builtin_nontemporal_load(&muy[p * nxy + ooff]);
-        }
+            if (own[v]) {   // (the old mu is dead after this kernel)
+                om[v][0] = __builtin_nontemporal_load(&mut[p * nxy + ooff[v]]);
+                om[v][1] = __builtin_nontemporal_load(&mux[p * nxy + ooff[v]]);
+                om[v][2] = __builtin_nontemporal_load(&muy[p * nxy + ooff[v]]);
+            }
 #else
-        if (own) { om[0] = mut[p * nxy + ooff]; om[1] = mux[p * nxy + ooff]; om[2] = muy[p * nxy + ooff]; }
+            if (own[v]) { om[v][0] = mut[p * nxy + ooff[v]]; om[v][1] = mux[p * nxy + ooff[v]]; om[v][2] = muy[p * nxy + ooff[v]]; }
 #endif
+        }
 #if FOTO_PR_NTLD >= 2
         if (hal) {
             hm[0] = __builtin_nontemporal_load(&mut[p * nxy + hoff]);
@@ -882,35 +903,40 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
         gyo = gy;
     };
     double num = 0.0, den = 0.0, ff = 0.0;
-    // own voxel: w_t of planes p-2, p-1, p; (mu'_t, q_t) of plane p-1 (bcm, bcq) and p (_n)
-    double wtm = 0.0, wtc = 0.0, wtn = 0.0, bcm = 0.0, bcq = 0.0, bcm_n = 0.0, bcq_n = 0.0;
-    // plane p's stepB for the own and the ring voxel: mu' out (own planes only), w into
+    // own voxels: w_t of planes p-2, p-1, p; (mu'_t, q_t) of plane p-1 (bcm, bcq) and p (_n)
+    double wtm[PR_VPT], wtc[PR_VPT], wtn[PR_VPT], bcm[PR_VPT], bcq[PR_VPT], bcm_n[PR_VPT], bcq_n[PR_VPT];
+#pragma unroll
+    for (int v = 0; v < PR_VPT; ++v) wtm[v] = wtc[v] = wtn[v] = bcm[v] = bcq[v] = bcm_n[v] = bcq_n[v] = 0.0;
+    // plane p's stepB for the own and the ring voxels: mu' out (own planes only), w into
     // wb[p & 1], crit terms (own planes only)
-    auto plane = [&](int p, const double (&mo)[3], const double (&mh)[3]) {
+    auto plane = [&](int p, const double (&mo)[PR_VPT][3], const double (&mh)[3]) {
         const bool mine = p >= l0 && p < l1;
-        if (own) {
-            double w[3], nu[3], n0, a, gt, gx, gy;
-            stepb(p, opx, opy, ox, oy, mo, w, n0, a, gt, gx, gy, nu);
-            if (mine) {
-                const int64_t i = p * nxy + ooff;
+#pragma unroll
+        for (int v = 0; v < PR_VPT; ++v) {
+            if (own[v]) {
+                double w[3], nu[3], n0, a, gt, gx, gy;
+                stepb(p, opx, opy[v], ox, oy[v], mo[v], w, n0, a, gt, gx, gy, nu);
+                if (mine) {
+                    const int64_t i = p * nxy + ooff[v];
 #if FOTO_PR_NT
-                __builtin_nontemporal_store(nu[0], &nut[i]);
-                __builtin_nontemporal_store(nu[1], &nux[i]);
-                __builtin_nontemporal_store(nu[2], &nuy[i]);
+                    __builtin_nontemporal_store(nu[0], &nut[i]);
+                    __builtin_nontemporal_store(nu[1], &nux[i]);
+                    __builtin_nontemporal_store(nu[2], &nuy[i]);
 #else
-                nut[i] = nu[0];
-                nux[i] = nu[1];
-                nuy[i] = nu[2];
+                    nut[i] = nu[0];
+                    nux[i] = nu[1];
+                    nuy[i] = nu[2];
 #endif
-                const double gg = gx * gx + gy * gy;
-                num += n0 * fabs(gt + 0.5 * gg);
-                den += n0 * gg;
+                    const double gg = gx * gx + gy * gy;
+                    num += n0 * fabs(gt + 0.5 * gg);
+                    den += n0 * gg;
+                }
+                wb[p & 1][0][opy[v] * PR_PW + opx] = w[1];
+                wb[p & 1][1][opy[v] * PR_PW + opx] = w[2];
+                wtn[v] = w[0];
+                bcm_n[v] = n0;
+                bcq_n[v] = a;
             }
-            wb[p & 1][0][opy * PR_PW + opx] = w[1];
-            wb[p & 1][1][opy * PR_PW + opx] = w[2];
-            wtn = w[0];
-            bcm_n = n0;
-            bcq_n = a;
         }
         if (hal) {
             double w[3], nu[3], n0, a, gt, gx, gy;
@@ -935,53 +961,63 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     for (int p = pa; p <= l1; ++p) {
         store_phi(p + 2);   // slot (p+2) & 3 = (p-2) & 3: last read by iteration p-1
         load_phi(p + 3);
-        const double cm[3] = {om[0], om[1], om[2]}, chm[3] = {hm[0], hm[1], hm[2]};   // mu(p)
+        double cm[PR_VPT][3];
+#pragma unroll
+        for (int v = 0; v < PR_VPT; ++v) { cm[v][0] = om[v][0]; cm[v][1] = om[v][1]; cm[v][2] = om[v][2]; }
+        const double chm[3] = {hm[0], hm[1], hm[2]};   // mu(p)
         load_mu(p + 1);
         if (p <= pz) plane(p, cm, chm);
-        else wtn = 0.0;   // t0 + p = Nt: F(Nt - 1) reads no w_t(Nt)
+        else {
+#pragma unroll
+            for (int v = 0; v < PR_VPT; ++v) wtn[v] = 0.0;   // t0 + p = Nt: F(Nt - 1) reads no w_t(Nt)
+        }
         const int n = p - 1, tn = t0 + n;
         const bool deferred = (defer_lo && n == 0) || (defer_hi && n == nl - 1);   // k_rhs_edge's
-        if (EDGE && own && n >= l0) {
-            // what k_rhs_edge needs next to a deferred edge, from the values F(n) would use: w_t
-            // of the two outermost planes, and (w_x, w_y, mu'_t, q_t) of the edge plane itself
-            if ((defer_lo && n <= 1) || (defer_hi && n >= nl - 2)) wt_out[n * nxy + ooff] = wtc;
-            if (deferred) {   // slot 0: plane 0, slot 1: plane nloc - 1 (nloc = 1: both)
-                const int ci = opy * PR_PW + opx;
-                double* E = edge + ooff + ((defer_lo && n == 0) ? 0 : 4 * nxy);
-                E[0] = wb[n & 1][0][ci];
-                E[nxy] = wb[n & 1][1][ci];
-                E[2 * nxy] = bcm;
-                E[3 * nxy] = bcq;
-                if (defer_lo && defer_hi && nl == 1) {
-                    E[4 * nxy] = E[0];
-                    E[5 * nxy] = E[nxy];
-                    E[6 * nxy] = bcm;
-                    E[7 * nxy] = bcq;
+#pragma unroll
+        for (int v = 0; v < PR_VPT; ++v) {
+            if (EDGE && own[v] && n >= l0) {
+                // what k_rhs_edge needs next to a deferred edge, from the values F(n) would use: w_t
+                // of the two outermost planes, and (w_x, w_y, mu'_t, q_t) of the edge plane itself
+                if ((defer_lo && n <= 1) || (defer_hi && n >= nl - 2)) wt_out[n * nxy + ooff[v]] = wtc[v];
+                if (deferred) {   // slot 0: plane 0, slot 1: plane nloc - 1 (nloc = 1: both)
+                    const int ci = opy[v] * PR_PW + opx;
+                    double* E = edge + ooff[v] + ((defer_lo && n == 0) ? 0 : 4 * nxy);
+                    E[0] = wb[n & 1][0][ci];
+                    E[nxy] = wb[n & 1][1][ci];
+                    E[2 * nxy] = bcm[v];
+                    E[3 * nxy] = bcq[v];
+                    if (defer_lo && defer_hi && nl == 1) {
+                        E[4 * nxy] = E[0];
+                        E[5 * nxy] = E[nxy];
+                        E[6 * nxy] = bcm[v];
+                        E[7 * nxy] = bcq[v];
+                    }
                 }
             }
-        }
-        if (own && n >= l0 && !deferred) {
-            // F(n) (k_rhs's order: t, x, y terms, then the boundary-plane corrections)
-            const double* WX = wb[n & 1][0];
-            const double* WY = wb[n & 1][1];
-            const int ci = opy * PR_PW + opx;
-            double s = 0.0;
-            acc_d1w(s, tn, Nt, wtm, wtc, wtn);
-            acc_d1w(s, ox, Nx, ox > 0 ? WX[ci - 1] : 0.0, WX[ci], ox < Nx - 1 ? WX[ci + 1] : 0.0);
-            acc_d1w(s, oy, Ny, oy > 0 ? WY[ci - PR_PW] : 0.0, WY[ci], oy < Ny - 1 ? WY[ci + PR_PW] : 0.0);
-            if (tn == 0) s -= (rho0[ooff] - bcm) + r * bcq;
-            if (tn == Nt - 1) s += (rhoT[ooff] - bcm) + r * bcq;
+            if (own[v] && n >= l0 && !deferred) {
+                // F(n) (k_rhs's order: t, x, y terms, then the boundary-plane corrections)
+                const double* WX = wb[n & 1][0];
+                const double* WY = wb[n & 1][1];
+                const int ci = opy[v] * PR_PW + opx;
+                const int oo = ooff[v], yv = oy[v];
+                double s = 0.0;
+                acc_d1w(s, tn, Nt, wtm[v], wtc[v], wtn[v]);
+                acc_d1w(s, ox, Nx, ox > 0 ? WX[ci - 1] : 0.0, WX[ci], ox < Nx - 1 ? WX[ci + 1] : 0.0);
+                acc_d1w(s, yv, Ny, yv > 0 ? WY[ci - PR_PW] : 0.0, WY[ci], yv < Ny - 1 ? WY[ci + PR_PW] : 0.0);
+                if (tn == 0) s -= (rho0[oo] - bcm[v]) + r * bcq[v];
+                if (tn == Nt - 1) s += (rhoT[oo] - bcm[v]) + r * bcq[v];
 #if FOTO_PR_NT >= 2
-            __builtin_nontemporal_store(s, &F[n * nxy + ooff]);
+                __builtin_nontemporal_store(s, &F[n * nxy + oo]);
 #else
-            F[n * nxy + ooff] = s;
+                F[n * nxy + oo] = s;
 #endif
-            ff += s * s;
+                ff += s * s;
+            }
+            wtm[v] = wtc[v];
+            wtc[v] = wtn[v];
+            bcm[v] = bcm_n[v];
+            bcq[v] = bcq_n[v];
         }
-        wtm = wtc;
-        wtc = wtn;
-        bcm = bcm_n;
-        bcq = bcq_n;
         __syncthreads();
     }
     double v[3] = {num, den, ff}, tot[3];

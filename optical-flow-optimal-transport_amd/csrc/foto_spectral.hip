@@ -3190,8 +3190,10 @@ struct SpecImpl {
     GqState* dgq2[2] = {nullptr, nullptr};   // their device addresses (coherent host memory)
     GqNodes* gqn = nullptr;
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
+    bool gq_nodes_wave = true;    // k_gq_nodes_w (FOTO_GQ_NODES=thread: k_gq_nodes, the round-4 form)
     double* gq_tab = nullptr;
     GqBins* gq_bins = nullptr;    // bin edges of the measure and the solution table
+    GqQCos* gq_qcos = nullptr;    // the solution table's transform constants
     // bin-ordered histogram (k_gq_hist_perm): the box's voxels grouped by bin, chunked
     unsigned* gq_permv = nullptr;
     GqChunk* gq_chunks = nullptr;
@@ -3429,12 +3431,16 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         }
         FOTO_TRY(P->alloc(sizeof(GqNodes), &b)); P->gqn = (GqNodes*)b;
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
+        const char* gn = getenv("FOTO_GQ_NODES");
+        P->gq_nodes_wave = !(gn && std::strcmp(gn, "thread") == 0);
         FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
         // k_gq_xhat holds the whole table (128 KB) in dynamic LDS, beside its 10 KB bin tables
         FOTO_HIP_CHECK(hipFuncSetAttribute((const void*)k_gq_xhat, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)GQ_TAB_BYTES));
         FOTO_TRY(P->alloc(sizeof(GqBins), &b)); P->gq_bins = (GqBins*)b;
         k_gq_bins<<<1, 256, 0, s>>>(P->gq_bins);
+        FOTO_TRY(P->alloc(sizeof(GqQCos), &b)); P->gq_qcos = (GqQCos*)b;
+        k_gq_qcos<<<1, 256, 0, s>>>(P->gq_qcos);
         FOTO_HIP_CHECK(hipGetLastError());
         FOTO_TRY(P->alloc(sizeof(GqExact), &b)); P->gq_exact = (GqExact*)b;
         FOTO_TRY(gq_build_perm(P, s));
@@ -3819,6 +3825,9 @@ static int tcol_inverse(SpecImpl* P, double* b, double* x, double rtol, int maxi
 }
 
 // ---------------------------------------------------------------------------- Gauss-compressed CG (host)
+// one shard, wave-per-bin nodes: k_gq_nodes_w sums the chunk sums itself (no histogram pass)
+static bool gq_fused_reduce(const SpecImpl* P) { return P->gq_nodes_wave && P->world == 1; }
+
 // b^ -> this box's histogram (slot rank of gq_hist)
 static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     const SpecTab T = P->tab();
@@ -3827,8 +3836,11 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     k_gq_hist_perm<<<nbk, 256, 0, s>>>(T, P->bh, P->gq_permv, P->gq_chunks, P->gq_nch, P->gq_bins, P->gq_exact,
                                        P->gq_rowmu, 1.0 / P->c1, P->gq_ppart);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_perm_reduce<<<GQ_HIST / 4, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
-    FOTO_HIP_CHECK(hipGetLastError());
+    // (one shard with the wave-per-bin node kernel: the bin sums are taken there, from the chunk sums)
+    if (!gq_fused_reduce(P)) {
+        k_gq_perm_reduce<<<GQ_HIST / 4, 256, 0, s>>>(P->gq_ppart, P->gq_cfirst, P->gq_hist + (size_t)P->rank * GQ_HIST);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 8.0 * P->nbox());
     return 0;
 }
@@ -3836,7 +3848,14 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
 // the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
 static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
-    k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->gq_exact, P->world, P->r * P->eps, P->c1, P->gqn);
+    if (!P->gq_nodes_wave)
+        k_gq_nodes<<<GQ_NODES / 64, 64, 0, s>>>(P->gq_hist, P->gq_bins, P->gq_exact, P->world, P->r * P->eps, P->c1, P->gqn);
+    else if (gq_fused_reduce(P))
+        k_gq_nodes_w<<<GQ_NB / 4, 256, 0, s>>>(nullptr, P->gq_ppart, P->gq_cfirst, P->gq_bins, P->gq_exact, 1,
+                                               P->r * P->eps, P->c1, P->gqn);
+    else
+        k_gq_nodes_w<<<GQ_NB / 4, 256, 0, s>>>(P->gq_hist, nullptr, nullptr, P->gq_bins, P->gq_exact, P->world,
+                                               P->r * P->eps, P->c1, P->gqn);
     FOTO_HIP_CHECK(hipGetLastError());
     const char* kl = getenv("FOTO_GQ_KLIM");   // (tests: force the s-step redo path)
     const int klim = kl ? std::max(0, std::min(GQ_KMAX, atoi(kl))) : GQ_KMAX;
@@ -3847,7 +3866,7 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
     const bool direct = !(hc && atoi(hc) == 0);
     k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq, direct ? P->dgq2[P->hlast] : nullptr);
     FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->r * P->eps, P->c1, P->gq_tab);
+    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->gq_qcos, P->r * P->eps, P->c1, P->gq_tab);
     FOTO_HIP_CHECK(hipGetLastError());
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
     if (!direct)

@@ -203,6 +203,220 @@ __global__ __launch_bounds__(NTH) void k_cg_noreduce(const GqNodes* __restrict__
     if (threadIdx.x == 0) S->rn2 = sa[0];
 }
 
+// ---- two steps per reduction (round 5).  At the top of a pair the lanes hold r = r_k and
+// a = A p_{k-1}; step k's alpha, beta come from rho = r.r and delta = r.Ar as in k_gq_cg, and
+// step k + 1's from the same reduction: r_{k+1} = (1 - alpha lam) r - alpha beta a, so
+//   rho'   = Srr  - 2 al Slrr  + al^2 Sl2rr - 2 al be (Sra  - al Slra)  + (al be)^2 Saa
+//   delta' = Slrr - 2 al Sl2rr + al^2 Sl3rr - 2 al be (Slra - al Sl2ra) + (al be)^2 Slaa
+// -- nine sums, one barrier per two steps.  RED 0: each sum by its own DPP tree (as reduce2);
+// RED 1: a butterfly reduce-scatter inside each 16-lane row (mirror, half-mirror, quad xor 2,
+// quad xor 1: 5 + 3 + 2 + 1 exchanges for the nine sums), then xor 16 / xor 32 by gfx950's
+// permlane swaps, the 4 waves' rows through LDS, and readlanes.
+constexpr int C2N = 9;
+__device__ __forceinline__ double dbl_pl16(double v) {   // v of lane l ^ 16
+    const long long b = __double_as_longlong(v);
+    const unsigned l = threadIdx.x & 63;
+    auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const unsigned rl = (l & 16) ? lo[0] : lo[1], rh = (l & 16) ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)rh << 32) | rl);
+}
+__device__ __forceinline__ double dbl_pl32(double v) {   // v of lane l ^ 32
+    const long long b = __double_as_longlong(v);
+    const unsigned l = threadIdx.x & 63;
+    auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+    auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const unsigned rl = (l & 32) ? lo[0] : lo[1], rh = (l & 32) ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)rh << 32) | rl);
+}
+template <int CIN, int CTRL>
+__device__ __forceinline__ void bfly(double (&v)[C2N], bool bit) {
+    constexpr int H = (CIN + 1) / 2;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const double lo = v[i], hi = (H + i < CIN) ? v[H + i] : 0.0;
+        const double send = bit ? lo : hi, keep = bit ? hi : lo;
+        v[i] = keep + dbl_dpp<CTRL>(send);
+    }
+}
+// the sum a row lane holds after the four stages (-1: padding), from the same halving
+struct BflyMap {
+    int lane_of[C2N];
+    constexpr BflyMap() : lane_of{} {
+        for (int l = 0; l < 16; ++l) {
+            const int bits[4] = {(l >> 3) & 1, (l >> 2) & 1, (l >> 1) & 1, l & 1};
+            const int cin[4] = {9, 5, 3, 2};
+            int base = 0, cnt = 9;
+            for (int st = 0; st < 4; ++st) {
+                const int H = (cin[st] + 1) / 2;
+                if (bits[st]) { base += H; cnt = cnt - H; }
+                else cnt = cnt < H ? cnt : H;
+            }
+            if (cnt >= 1 && base < C2N) lane_of[base] = l;
+        }
+    }
+};
+constexpr BflyMap BFLY{};
+
+template <int RED>
+__global__ __launch_bounds__(256) void k_cg2(const GqNodes* __restrict__ nd, double rtol, int maxiter, int klim,
+                                             GqState* __restrict__ S) {
+    constexpr int NTH = 256, NW = 4, NPT = GQ_NODES / NTH;
+    __shared__ __attribute__((aligned(16))) double red[2][NW][16];
+    __shared__ double abL[2][GQ_KMAX];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double lam[NPT], r[NPT], a[NPT];
+    double mass = 0.0;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+        const int id = threadIdx.x * NPT + j;
+        lam[j] = nd->lam[id];
+        const double w = nd->w[id];
+        r[j] = sqrt(w);
+        a[j] = 0.0;
+        mass += w;
+    }
+    auto sums = [&](double (&s)[C2N]) {
+#pragma unroll
+        for (int q = 0; q < C2N; ++q) s[q] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            const double lr = lam[j] * r[j], la = lam[j] * a[j], lr2 = lr * lr;
+            s[0] = fma(r[j], r[j], s[0]);
+            s[1] = fma(lr, r[j], s[1]);
+            s[2] += lr2;
+            s[3] = fma(lam[j], lr2, s[3]);
+            s[4] = fma(r[j], a[j], s[4]);
+            s[5] = fma(lr, a[j], s[5]);
+            s[6] = fma(lr, la, s[6]);
+            s[7] = fma(a[j], a[j], s[7]);
+            s[8] = fma(la, a[j], s[8]);
+        }
+    };
+    // block totals of v[0 .. C2N), the same bits in every lane
+    auto reduce9 = [&](double (&v)[C2N], int slot, double (&t)[C2N]) {
+        if constexpr (RED == 0) {
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp<0x111>(v[q]);
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp<0x112>(v[q]);
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp<0x114>(v[q]);
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp<0x118>(v[q]);
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp_rows<0x142, 0xa>(v[q]);
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) v[q] += dbl_dpp_rows<0x143, 0xc>(v[q]);
+            if (lane == 63) {
+#pragma unroll
+                for (int q = 0; q < C2N; ++q) red[slot][wv][q] = v[q];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) {
+                double x = red[slot][0][q];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) x += red[slot][w][q];
+                t[q] = x;
+            }
+        } else {
+            const int l = lane & 15;
+            bfly<9, 0x140>(v, (l >> 3) & 1);   // row_mirror: l <-> 15 - l
+            bfly<5, 0x141>(v, (l >> 2) & 1);   // row_half_mirror: l <-> 7 - l in each half row
+            bfly<3, 0x4E>(v, (l >> 1) & 1);    // quad_perm [2, 3, 0, 1]
+            bfly<2, 0xB1>(v, l & 1);           // quad_perm [1, 0, 3, 2]
+            double x = v[0];
+            x += dbl_pl16(x);
+            x += dbl_pl32(x);
+            if (lane < 16) red[slot][wv][lane] = x;
+            __syncthreads();
+            double y = red[slot][0][l];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) y += red[slot][w][l];
+#pragma unroll
+            for (int q = 0; q < C2N; ++q) t[q] = dbl_readlane(y, BFLY.lane_of[q]);
+        }
+    };
+    double tt[C2N], ss[C2N];
+    {
+        double m[C2N];
+#pragma unroll
+        for (int q = 0; q < C2N; ++q) m[q] = 0.0;
+        m[0] = mass;
+        reduce9(m, 1, tt);
+    }
+    const double bn2 = tt[0];
+    const double atol = rtol * sqrt(bn2);
+    const double atol2 = atol * atol;
+    int status = 0, conv = 0, K = maxiter;
+    double rho = bn2, irho_prev = 1.0, sigma_prev = 1.0;
+    auto rdiv = [](double num, double den) {
+        double y = __builtin_amdgcn_rcp(den);
+        y = fma(y, fma(-den, y, 1.0), y);
+        y = fma(y, fma(-den, y, 1.0), y);
+        double q = num * y;
+        return fma(fma(-den, q, num), y, q);
+    };
+    sums(ss);
+    for (int k = 0; k < maxiter; k += 2) {
+        reduce9(ss, (k >> 1) & 1, tt);
+        rho = tt[0];
+        const double delta = tt[1];
+        if (rho < atol2) { K = k; conv = 1; break; }
+        if (k >= klim) { K = k; status = 2; break; }
+        const double beta = (k == 0) ? 0.0 : rho * irho_prev;
+        const double sigma = (k == 0) ? delta : fma(-beta * beta, sigma_prev, delta);
+        if (!(sigma > 0.0) || !isfinite(sigma)) { K = k; status = 1; break; }
+        const double alpha = rdiv(rho, sigma);
+        if (threadIdx.x == 0) { abL[0][k] = alpha; abL[1][k] = beta; }
+        const double ab = alpha * beta, ab2 = ab * ab, a2 = alpha * alpha;
+        const double rho1 = fma(ab2, tt[7], fma(-2.0 * ab, fma(-alpha, tt[5], tt[4]), fma(a2, tt[2], fma(-2.0 * alpha, tt[1], tt[0]))));
+        const double delta1 = fma(ab2, tt[8], fma(-2.0 * ab, fma(-alpha, tt[6], tt[5]), fma(a2, tt[3], fma(-2.0 * alpha, tt[2], tt[1]))));
+        // step k + 1 (unless the pair ends after step k)
+        int fin = 0;   // 1: K = k + 1 after step k's update
+        double beta1 = 0.0, alpha1 = 0.0, sigma1 = 0.0;
+        if (k + 1 >= maxiter) { fin = 1; K = k + 1; rho = rho; }
+        else if (rho1 < atol2) { fin = 1; K = k + 1; conv = 1; rho = rho1; }
+        else if (k + 1 >= klim) { fin = 1; K = k + 1; status = 2; rho = rho1; }
+        else {
+            beta1 = rho1 * (1.0 / rho);
+            sigma1 = fma(-beta1 * beta1, sigma, delta1);
+            if (!(sigma1 > 0.0) || !isfinite(sigma1)) { fin = 1; K = k + 1; status = 1; rho = rho1; }
+            else alpha1 = rdiv(rho1, sigma1);
+        }
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            a[j] = fma(beta, a[j], lam[j] * r[j]);
+            r[j] = fma(-alpha, a[j], r[j]);
+        }
+        if (fin) break;
+        if (threadIdx.x == 0) { abL[0][k + 1] = alpha1; abL[1][k + 1] = beta1; }
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            a[j] = fma(beta1, a[j], lam[j] * r[j]);
+            r[j] = fma(-alpha1, a[j], r[j]);
+        }
+        rho = rho1;
+        irho_prev = 1.0 / rho1;
+        sigma_prev = sigma1;
+        sums(ss);
+    }
+    __syncthreads();
+    const int kst = (K < GQ_KMAX) ? K : GQ_KMAX;
+    for (int e = threadIdx.x; e < kst; e += NTH) {
+        S->alpha[e] = abL[0][e];
+        S->beta[e] = abL[1][e];
+    }
+    if (threadIdx.x == 0) {
+        S->K = K;
+        S->status = status;
+        S->conv = conv;
+        S->bn2 = bn2;
+        S->rn2 = rho;
+    }
+}
+
 #define CK(x)                                                                          \
     do {                                                                               \
         hipError_t e_ = (x);                                                           \
@@ -271,6 +485,24 @@ int main(int argc, char** argv) {
     timeit("lr/ap 256 bcast nacc8", [&] { k_cg_var<256, 1, 8><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
     timeit("lr/ap 512 rows-LDS", [&] { k_cg_var<512, 2><<<1, 512>>>(nd, 0.0, maxiter, S1); }, true);
     timeit("lr/ap 512 bcast", [&] { k_cg_var<512, 1><<<1, 512>>>(nd, 0.0, maxiter, S1); }, true);
+    timeit("2-step naive DPP", [&] { k_cg2<0><<<1, 256>>>(nd, 0.0, maxiter, GQ_KMAX, S1); }, true);
+    timeit("2-step butterfly", [&] { k_cg2<1><<<1, 256>>>(nd, 0.0, maxiter, GQ_KMAX, S1); }, true);
+    {   // with a stop test: the iteration count against the product's
+        const double rtols[3] = {1e-3, 1e-5, 1e-7};
+        for (double rt : rtols) {
+            k_gq_cg<<<1, GQ_CGNTH>>>(nd, rt, 100000, GQ_KMAX, S0, nullptr);
+            k_cg2<1><<<1, 256>>>(nd, rt, 100000, GQ_KMAX, S1);
+            CK(hipMemcpy(&h0, S0, sizeof(GqState), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&h1, S1, sizeof(GqState), hipMemcpyDeviceToHost));
+            double err = 0;
+            for (int k = 0; k < std::min(h0.K, h1.K) && k < GQ_KMAX; ++k) {
+                err = std::max(err, fabs(h1.alpha[k] - h0.alpha[k]) / fabs(h0.alpha[k]));
+                if (k) err = std::max(err, fabs(h1.beta[k] - h0.beta[k]) / fabs(h0.beta[k]));
+            }
+            printf("  rtol %.0e: product K %d conv %d status %d rn2 %.6e | 2-step K %d conv %d status %d rn2 %.6e | d(alpha,beta) %.2e\n",
+                   rt, h0.K, h0.conv, h0.status, h0.rn2, h1.K, h1.conv, h1.status, h1.rn2, err);
+        }
+    }
     timeit("no reduction 64", [&] { k_cg_noreduce<64><<<1, 64>>>(nd, maxiter, S1); }, false);
     timeit("no reduction 128", [&] { k_cg_noreduce<128><<<1, 128>>>(nd, maxiter, S1); }, false);
     timeit("no reduction 512", [&] { k_cg_noreduce<512><<<1, 512>>>(nd, maxiter, S1); }, false);

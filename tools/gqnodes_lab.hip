@@ -106,20 +106,31 @@ int main(int argc, char** argv) {
     }
     const double lmin = 1e-2, c1 = 6.0;   // lam = lmin + c1 s, s in [0, 2]
     std::vector<double> hist(GQ_HIST, 0.0);
+    // chunk sums too (k_gq_hist_perm's output: [chunk][moment], chunks of a bin consecutive),
+    // 8 .. 71 chunks per bin, for k_gq_nodes_w's fused reduction
+    std::vector<int> cfirst(GQ_NB + 1, 0);
+    std::vector<double> part;
     srand(11);
     for (int b = 0; b < GQ_NB; ++b) {
         const double mid = 0.5 * (hi[b] + hi[b + 1]), hw = 0.5 * (hi[b] - hi[b + 1]);
         const int np = 200 + rand() % 400;
+        const int nch = 8 + rand() % 64;
+        cfirst[b + 1] = cfirst[b] + nch;
+        part.resize((size_t)cfirst[b + 1] * GQ_NM, 0.0);
         for (int q = 0; q < np; ++q) {
+            double* pc = &part[(size_t)(cfirst[b] + q % nch) * GQ_NM];
             const double u = 2.0 * rand() / (double)RAND_MAX - 1.0;
             const double s = mid + hw * u, lam = lmin + c1 * s;
             const double w = exp(-decay * lam) * (0.1 + rand() / (double)RAND_MAX);
             double tm2 = 1.0, tm1 = u;
             hist[0 * GQ_NB + b] += w;
             hist[1 * GQ_NB + b] += w * u;
+            pc[0] += w;
+            pc[1] += w * u;
             for (int m = 2; m < GQ_NM; ++m) {
                 const double t = 2.0 * u * tm1 - tm2;
                 hist[m * GQ_NB + b] += w * t;
+                pc[m] += w * t;
                 tm2 = tm1;
                 tm1 = t;
             }
@@ -152,6 +163,62 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, e));
     printf("k_gq_nodes: %.2f us per launch (decay %.1f)\n", 1e3 * ms / reps, decay);
+    // the wave-per-bin form, from the histogram and from the chunk sums (+ k_gq_perm_reduce's
+    // output for the bitwise check of the fused reduction)
+    {
+        double *dpart, *dh2;
+        int* dcf;
+        GqNodes* nd2;
+        GqNodes* nd3;
+        const int nch = cfirst[GQ_NB];
+        CK(hipMalloc(&dpart, sizeof(double) * part.size()));
+        CK(hipMalloc(&dh2, sizeof(double) * GQ_HIST));
+        CK(hipMalloc(&dcf, sizeof(int) * (GQ_NB + 1)));
+        CK(hipMalloc(&nd2, sizeof(GqNodes)));
+        CK(hipMalloc(&nd3, sizeof(GqNodes)));
+        CK(hipMemcpy(dpart, part.data(), sizeof(double) * part.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(dcf, cfirst.data(), sizeof(int) * (GQ_NB + 1), hipMemcpyHostToDevice));
+        k_gq_perm_reduce<<<GQ_HIST / 4, 256>>>(dpart, dcf, dh2);
+        k_gq_nodes<<<GQ_NODES / 64, 64>>>(dh2, B, X, 1, lmin, c1, nd);
+        k_gq_nodes_w<<<GQ_NB / 4, 256>>>(dh2, nullptr, nullptr, B, X, 1, lmin, c1, nd2);
+        k_gq_nodes_w<<<GQ_NB / 4, 256>>>(nullptr, dpart, dcf, B, X, 1, lmin, c1, nd3);
+        CK(hipDeviceSynchronize());
+        std::vector<double> l1(GQ_NODES), w1(GQ_NODES), l2(GQ_NODES), w2(GQ_NODES), l3(GQ_NODES), w3(GQ_NODES);
+        CK(hipMemcpy(l1.data(), nd->lam, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(w1.data(), nd->w, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(l2.data(), nd2->lam, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(w2.data(), nd2->w, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(l3.data(), nd3->lam, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(w3.data(), nd3->w, sizeof(double) * GQ_NODES, hipMemcpyDeviceToHost));
+        double dl = 0, dw = 0;
+        int same23 = 1, nz = 0;
+        for (int i = 0; i < GQ_NODES; ++i) {
+            dl = std::max(dl, fabs(l2[i] - l1[i]) / fabs(l1[i]));
+            if (w1[i] != 0.0) dw = std::max(dw, fabs(w2[i] - w1[i]) / fabs(w1[i]));
+            nz += (w1[i] != 0.0);
+            same23 &= (l2[i] == l3[i] && w2[i] == w3[i]);
+        }
+        printf("nodes_w vs nodes: max rel d lam %.2e, d w %.2e (%d weighted nodes); fused reduction bitwise %s\n",
+               dl, dw, nz, same23 ? "equal" : "DIFFERENT");
+        for (int pass = 0; pass < 2; ++pass) {
+            CK(hipEventRecord(a, 0));
+            for (int i = 0; i < reps; ++i) {
+                if (pass == 0) k_gq_nodes_w<<<GQ_NB / 4, 256>>>(dh2, nullptr, nullptr, B, X, 1, lmin, c1, nd2);
+                else k_gq_nodes_w<<<GQ_NB / 4, 256>>>(nullptr, dpart, dcf, B, X, 1, lmin, c1, nd3);
+            }
+            CK(hipEventRecord(e, 0));
+            CK(hipEventSynchronize(e));
+            CK(hipEventElapsedTime(&ms, a, e));
+            printf("k_gq_nodes_w (%s): %.2f us per launch\n", pass ? "chunk sums, fused reduction" : "histogram",
+                   1e3 * ms / reps);
+        }
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < reps; ++i) k_gq_perm_reduce<<<GQ_HIST / 4, 256>>>(dpart, dcf, dh2);
+        CK(hipEventRecord(e, 0));
+        CK(hipEventSynchronize(e));
+        CK(hipEventElapsedTime(&ms, a, e));
+        printf("k_gq_perm_reduce: %.2f us per launch (%d chunks)\n", 1e3 * ms / reps, nch);
+    }
     long long* clk;
     CK(hipMalloc(&clk, 4 * sizeof(long long)));
     k_nodes_count<<<GQ_NODES / 64, 64>>>(dh, X, cnt, clk);
