@@ -197,6 +197,40 @@ __device__ __forceinline__ void gn_row(const GNPix& P, int w, int64_t n, int64_t
     (void)n;
 }
 
+// gn_row with the five stencil values of each field already fetched: V(f, k), k in CSR order
+// (y-1, x-1, centre, x+1, y+1; missing neighbours fetched at the centre's index, as gn_lap_row
+// does) -- the same additions in the same order
+template <class F>
+__device__ __forceinline__ double gn_lap_row_v(const GNPix& P, double coef, double dg, F val, double s) {
+    const double m = -coef;
+    s = P.hy ? s + m * val(0) : s;
+    s = P.hx ? s + m * val(1) : s;
+    s += dg * val(2);
+    s = P.hX ? s + m * val(3) : s;
+    s = P.hY ? s + m * val(4) : s;
+    return s;
+}
+
+template <class F>
+__device__ __forceinline__ void gn_row_v(const GNPix& P, double fx, double fy, double f2, double a, double l, F val,
+                                         double& yu, double& yv, double& ym) {
+    const double ui = val(0, 2), vi = val(1, 2), mi = val(2, 2);
+    double s = gn_lap_row_v(P, a, a * P.c + fx * fx, [&](int k) { return val(0, k); }, 0.0);
+    s += (fx * fy) * vi;
+    s += (-fx * f2) * mi;
+    yu = s;
+    s = 0.0;
+    s += (fy * fx) * ui;
+    s = gn_lap_row_v(P, a, a * P.c + fy * fy, [&](int k) { return val(1, k); }, s);
+    s += (-fy * f2) * mi;
+    yv = s;
+    s = 0.0;
+    s += (-f2 * fx) * ui;
+    s += (-f2 * fy) * vi;
+    s = gn_lap_row_v(P, l, l * P.c + f2 * f2, [&](int k) { return val(2, k); }, s);
+    ym = s;
+}
+
 __global__ __launch_bounds__(NT) void k_gn_apply(int w, int h, const double* __restrict__ fx,
                                                  const double* __restrict__ fy, const double* __restrict__ f2,
                                                  double a, double l, const double* __restrict__ x,
@@ -428,6 +462,39 @@ __device__ __forceinline__ void mg_dinv(const MGLev& L, int64_t i, double r0, do
     z2 = d02 * r0 + d12 * r1 + d22 * r2;
 }
 
+// the cell's 6 coefficient planes (B or Dinv: xx xy xm yy ym mm) into registers
+__device__ __forceinline__ void mg_load6(const double* __restrict__ P, int64_t n, int64_t i, double (&c)[6]) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c[k] = P[k * n + i];
+}
+
+// mg_dinv with the cell's inverse block already in registers (the same arithmetic)
+__device__ __forceinline__ void mg_dinv_v(const double (&d)[6], double r0, double r1, double r2, double& z0,
+                                          double& z1, double& z2) {
+    z0 = d[0] * r0 + d[1] * r1 + d[2] * r2;
+    z1 = d[1] * r0 + d[3] * r1 + d[4] * r2;
+    z2 = d[2] * r0 + d[4] * r1 + d[5] * r2;
+}
+
+// (A x) of cell (x, y) with the cell's B in registers (mg_apply_t's arithmetic)
+template <class F>
+__device__ __forceinline__ void mg_apply_b(const MGLev& L, int x, int y, const double (&B)[6], F X, double& a0,
+                                           double& a1, double& a2, double& v0, double& v1, double& v2) {
+    const bool hxm = x > 0, hxp = x < L.w - 1, hym = y > 0, hyp = y < L.h - 1;
+    const double c = (double)((int)hxm + (int)hxp + (int)hym + (int)hyp);
+    double v[3], nb[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        v[f] = X(f, 0, 0);
+        nb[f] = (hxm ? X(f, 0, -1) : 0.0) + (hxp ? X(f, 0, 1) : 0.0) + (hym ? X(f, -1, 0) : 0.0) +
+                (hyp ? X(f, 1, 0) : 0.0);
+    }
+    a0 = L.s0 * (c * v[0] - nb[0]) + B[0] * v[0] + B[1] * v[1] + B[2] * v[2];
+    a1 = L.s1 * (c * v[1] - nb[1]) + B[1] * v[0] + B[3] * v[1] + B[4] * v[2];
+    a2 = L.s2 * (c * v[2] - nb[2]) + B[2] * v[0] + B[4] * v[1] + B[5] * v[2];
+    v0 = v[0]; v1 = v[1]; v2 = v[2];
+}
+
 // (A x) of cell (x, y) = global index i, with the vector in an LDS tile: X(f, dy, dx) is the
 // value at the neighbour offset (dy, dx) in {-1, 0, 1}; neighbours outside the grid are skipped
 template <class F>
@@ -518,9 +585,28 @@ __global__ __launch_bounds__(NT) void k_gnp_dir(int w, int h, const double* __re
                                                 const double* __restrict__ po, double* __restrict__ pn, CGScal* S,
                                                 const double* rr_part, int nb_rr, const double* rz_cur,
                                                 const double* rz_prev, int nb_rz, double* __restrict__ pq_part,
-                                                double rtol) {
-    if (S->done) return;
+                                                double rtol, double* __restrict__ qout, const double* rr_part2,
+                                                int nb_rr2) {
+    // (round 5) the stencil values of z and p_{k-1} and the pixel's coefficients are loaded before
+    // the partial sums that give beta, so the two waits overlap
     const int k = S->pad[0];
+    const int done = S->done;
+    const int64_t n = (int64_t)w * h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    const bool in = i < n;
+    const GNPix P = gn_pix(w, h, in ? i : 0);
+    double zv[3][5], pv5[3][5], cfx = 0.0, cfy = 0.0, cf2 = 0.0;
+    {
+        const int64_t j5[5] = {P.hy ? i - w : i, P.hx ? i - 1 : i, i, P.hX ? i + 1 : i, P.hY ? i + w : i};
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                zv[f][q] = in ? z[f * n + j5[q]] : 0.0;
+                pv5[f][q] = (in && k > 0) ? po[f * n + j5[q]] : 0.0;
+            }
+        if (in) { cfx = fx[i]; cfy = fy[i]; cf2 = f2[i]; }
+    }
     double rr, rzc, rzp;
     {
         const double* src[2] = {rz_cur, rz_prev};
@@ -528,12 +614,16 @@ __global__ __launch_bounds__(NT) void k_gnp_dir(int w, int h, const double* __re
         mg_sum_partials<2>(src, nb_rz, o);
         rzc = o[0];
         rzp = o[1];
-        const double* s1[1] = {rr_part};
+        // r.r of r_k: k_gnp_init's partials at k = 0, then the update's (k_gnp_upd, or the level-0
+        // down leg with the update folded in: rr_part2, one partial per tile)
+        const bool second = rr_part2 && k > 0;
+        const double* s1[1] = {second ? rr_part2 : rr_part};
         double o1[1];
         __syncthreads();   // mg_sum_partials' LDS is reused
-        mg_sum_partials<1>(s1, nb_rr, o1);
+        mg_sum_partials<1>(s1, second ? nb_rr2 : nb_rr, o1);
         rr = o1[0];
     }
+    if (done) return;
     const double atol = (k == 0) ? fmax(0.0, rtol * sqrt(rr)) : S->atol;
     if (rr == 0.0 || sqrt(rr) < atol) {
         if (blockIdx.x == 0 && threadIdx.x == 0) { S->done = 1; S->iters = k; }
@@ -541,19 +631,14 @@ __global__ __launch_bounds__(NT) void k_gnp_dir(int w, int h, const double* __re
     }
     if (k == 0 && blockIdx.x == 0 && threadIdx.x == 0) { S->bb = rr; S->atol = atol; }
     const double beta = (k > 0) ? rzc / rzp : 0.0;
-    const int64_t n = (int64_t)w * h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
     double pq = 0.0;
-    if (i < n) {
-        const GNPix P = gn_pix(w, h, i);
-        auto pv = [&](int f, int64_t j) -> double {
-            const int64_t o = f * n + j;
-            return (k == 0) ? z[o] : beta * po[o] + z[o];
-        };
+    if (in) {
+        auto pv = [&](int f, int q) -> double { return (k == 0) ? zv[f][q] : beta * pv5[f][q] + zv[f][q]; };
         double qu, qv, qm;
-        gn_row(P, w, n, i, fx[i], fy[i], f2[i], a, l, pv, qu, qv, qm);
-        const double pu = pv(0, i), pvv = pv(1, i), pm = pv(2, i);
+        gn_row_v(P, cfx, cfy, cf2, a, l, pv, qu, qv, qm);
+        const double pu = pv(0, 2), pvv = pv(1, 2), pm = pv(2, 2);
         pn[i] = pu; pn[n + i] = pvv; pn[2 * n + i] = pm;
+        if (qout) { qout[i] = qu; qout[n + i] = qv; qout[2 * n + i] = qm; }   // (the folded update's A p)
         pq = pu * qu + pvv * qv + pm * qm;
     }
     mg_block_partial(pq, pq_part);
@@ -666,42 +751,141 @@ __global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Di
     Dinv[5 * n + i] = c22 * id;
 }
 
+// k_gnp_upd folded into the level-0 down leg (round 5; FOTO_GN_FOLD=0: the separate kernel):
+// alpha = rz_k / p.q from the same consumer-side sums, r' = r - alpha q on the tile and its halo
+// (q = A p as k_gnp_dir computed it -- the values k_gnp_upd recomputes, bit for bit), x += alpha p
+// and r' stored on the tile, and the partial r'.r' per tile.  r is double-buffered by iteration
+// parity: the neighbouring tiles still read the old r of their halo cells.
+struct MGUpd {
+    const double* rold;
+    double* rnew;
+    const double* q;
+    const double* p;
+    double* x;
+    const double* rz_cur;
+    const double* pq_part;
+    double* rr_part;
+    CGScal* S;
+    int nb_rz, nb_pq;
+};
+
 // Down leg of one level, one GT_Y x GT_X fine tile per block:
 //   x = omega D^-1 f (pre-smoothing from zero) over the tile + 2 halo cells   -> LDS
 //   r = f - A x over the tile + 1 halo cell                                   -> LDS; x -> xg
 //   fc = R r = P^T r / 4 for the tile's GT_Y/2 x GT_X/2 coarse cells (4 x 4 taps) -> fc
+// UPD (level 0 of a PCG iteration): f is r' = r - alpha q, formed here (MGUpd above)
+template <bool UPD>
 __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const CGScal* S,
                                                  const double* __restrict__ f, double* __restrict__ xg,
-                                                 double* __restrict__ fc) {
-    if (S->done) return;
+                                                 double* __restrict__ fc, MGUpd U) {
+    // Every global load of the first two stages is issued up front (round 5): a small level's
+    // launch was three dependent memory round trips (the done flag, f and D^-1, then B and f
+    // again) at 7-8 us for 1-40 tiles.  f of the region goes to LDS for the second stage.
     constexpr int XW = GT_X + 4, XH = GT_Y + 4, RW = GT_X + 2, RH = GT_Y + 2;
+    constexpr int C1 = (XH * XW + NT - 1) / NT, C2 = (RH * RW + NT - 1) / NT;
     __shared__ double xs[3][XH][XW];
+    __shared__ double fs[3][XH][XW];
     __shared__ double rs[3][RH][RW];
+    const int done = S->done;
     const int w = L.w, h = L.h;
     const int64_t n = (int64_t)w * h;
     const int tiles_x = (w + GT_X - 1) / GT_X;
     const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
-    for (int c = threadIdx.x; c < XH * XW; c += NT) {
+    // stage-2 cells' B (tile + 1 halo)
+    double b2[C2][6];
+#pragma unroll
+    for (int k = 0; k < C2; ++k) {
+        const int c = threadIdx.x + k * NT;
+        const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+        if (c < RH * RW && gx >= 0 && gx < w && gy >= 0 && gy < h) mg_load6(L.B, n, (int64_t)gy * w + gx, b2[k]);
+        else { for (int q = 0; q < 6; ++q) b2[k][q] = 0.0; }
+    }
+    // stage-1 cells' f (UPD: r and q) and D^-1 (tile + 2 halo)
+    double f1[C1][3], d1[C1][6];
+#pragma unroll
+    for (int k = 0; k < C1; ++k) {
+        const int c = threadIdx.x + k * NT;
+        const int ly = c / XW, lx = c - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
+        if (c < XH * XW && gx >= 0 && gx < w && gy >= 0 && gy < h) {
+            const int64_t i = (int64_t)gy * w + gx;
+            if constexpr (UPD) {
+                f1[k][0] = U.rold[i]; f1[k][1] = U.rold[n + i]; f1[k][2] = U.rold[2 * n + i];
+            } else {
+                f1[k][0] = f[i]; f1[k][1] = f[n + i]; f1[k][2] = f[2 * n + i];
+            }
+            mg_load6(L.Dinv, n, i, d1[k]);
+        } else {
+            f1[k][0] = f1[k][1] = f1[k][2] = 0.0;
+            for (int q = 0; q < 6; ++q) d1[k][q] = 0.0;
+        }
+    }
+    double alpha = 0.0;
+    if constexpr (UPD) {   // r' = r - alpha q (k_gnp_upd's expression); alpha = rz_k / p.q
+        double qv[C1][3];
+#pragma unroll
+        for (int k = 0; k < C1; ++k) {
+            const int c = threadIdx.x + k * NT;
+            const int ly = c / XW, lx = c - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
+            const bool in = c < XH * XW && gx >= 0 && gx < w && gy >= 0 && gy < h;
+            const int64_t i = in ? (int64_t)gy * w + gx : 0;
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) qv[k][fl] = in ? U.q[fl * n + i] : 0.0;
+        }
+        const double* s1[1] = {U.rz_cur};
+        double o1[1];
+        mg_sum_partials<1>(s1, U.nb_rz, o1);
+        const double* s2[1] = {U.pq_part};
+        double o2[1];
+        __syncthreads();
+        mg_sum_partials<1>(s2, U.nb_pq, o2);
+        alpha = o1[0] / o2[0];
+#pragma unroll
+        for (int k = 0; k < C1; ++k)
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) f1[k][fl] = f1[k][fl] - alpha * qv[k][fl];
+    }
+    if (done) return;   // (uniform; the loads above were issued before this wait)
+#pragma unroll
+    for (int k = 0; k < C1; ++k) {
+        const int c = threadIdx.x + k * NT;
+        if (c >= XH * XW) continue;
         const int ly = c / XW, lx = c - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
         double z0 = 0.0, z1 = 0.0, z2 = 0.0;
         if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
-            const int64_t i = (int64_t)gy * w + gx;
-            mg_dinv(L, i, f[i], f[n + i], f[2 * n + i], z0, z1, z2);
+            mg_dinv_v(d1[k], f1[k][0], f1[k][1], f1[k][2], z0, z1, z2);
             z0 *= MG_OMEGA; z1 *= MG_OMEGA; z2 *= MG_OMEGA;
         }
         xs[0][ly][lx] = z0; xs[1][ly][lx] = z1; xs[2][ly][lx] = z2;
+        fs[0][ly][lx] = f1[k][0]; fs[1][ly][lx] = f1[k][1]; fs[2][ly][lx] = f1[k][2];
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < RH * RW; c += NT) {
+    double rr = 0.0;
+#pragma unroll
+    for (int k = 0; k < C2; ++k) {
+        const int c = threadIdx.x + k * NT;
+        if (c >= RH * RW) continue;
         const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
         double r0 = 0.0, r1 = 0.0, r2 = 0.0;
         if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
             const int64_t i = (int64_t)gy * w + gx;
             double a0, a1, a2, v0, v1, v2;
-            mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0, a1,
-                       a2, v0, v1, v2);
-            r0 = f[i] - a0; r1 = f[n + i] - a1; r2 = f[2 * n + i] - a2;
-            if (ly >= 1 && ly <= GT_Y && lx >= 1 && lx <= GT_X) { xg[i] = v0; xg[n + i] = v1; xg[2 * n + i] = v2; }
+            mg_apply_b(L, gx, gy, b2[k], [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0,
+                       a1, a2, v0, v1, v2);
+            const double fa = fs[0][ly + 1][lx + 1], fb = fs[1][ly + 1][lx + 1], fcv = fs[2][ly + 1][lx + 1];
+            r0 = fa - a0; r1 = fb - a1; r2 = fcv - a2;
+            if (ly >= 1 && ly <= GT_Y && lx >= 1 && lx <= GT_X) {
+                xg[i] = v0; xg[n + i] = v1; xg[2 * n + i] = v2;
+                if constexpr (UPD) {   // k_gnp_upd's stores and its r.r terms, field order
+                    const double fr[3] = {fa, fb, fcv};
+#pragma unroll
+                    for (int fl = 0; fl < 3; ++fl) {
+                        const int64_t o = fl * n + i;
+                        U.x[o] = U.x[o] + alpha * U.p[o];
+                        U.rnew[o] = fr[fl];
+                        rr += fr[fl] * fr[fl];
+                    }
+                }
+            }
         }
         rs[0][ly][lx] = r0; rs[1][ly][lx] = r1; rs[2][ly][lx] = r2;
     }
@@ -721,26 +905,33 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int dy = 0; dy < 4; ++dy) {
-            double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+            double b0 = 0.0, b1 = 0.0, bb = 0.0;
 #pragma unroll
             for (int dx = 0; dx < 4; ++dx) {
                 const int ly = 2 * cy + dy, lx = 2 * cx + dx;   // (2J - 1 + dy) - (y0 - 1)
                 b0 += wx[dx] * rs[0][ly][lx];
                 b1 += wx[dx] * rs[1][ly][lx];
-                b2 += wx[dx] * rs[2][ly][lx];
+                bb += wx[dx] * rs[2][ly][lx];
             }
-            a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * b2;
+            a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * bb;
         }
         const int64_t I = (int64_t)J * wc + K;
         fc[I] = 0.25 * a0;
         fc[nc + I] = 0.25 * a1;
         fc[2 * nc + I] = 0.25 * a2;
     }
+    if constexpr (UPD) {
+        mg_block_partial(rr, U.rr_part);
+        // the iteration index: read by k_gnp_dir only, so no block of this launch races with it
+        if (blockIdx.x == 0 && threadIdx.x == 0) U.S->pad[0] = U.S->pad[0] + 1;
+    }
 }
 
 // Up leg of one level, one GT_Y x GT_X fine tile per block:
 //   x' = x + P ec over the tile + 1 halo cell -> LDS
 //   out = x' + omega D^-1 (f - A x') on the tile; RZ: partial f . out -> rz_part[block]
+// (Round 5: this kernel's B, f and D^-1 loaded before the prolongation stage, as k_mg_down2 does,
+// measured 0.2-1.2 us slower per launch at every level -- not kept.)
 template <bool RZ>
 __global__ __launch_bounds__(NT) void k_mg_up2(MGLev L, int wc, int hc, const CGScal* S,
                                                const double* __restrict__ ec, const double* __restrict__ f,
@@ -793,58 +984,75 @@ __global__ __launch_bounds__(NT) void k_mg_up2(MGLev L, int wc, int hc, const CG
 }
 
 // coarsest level: MG_CSWEEPS damped block-Jacobi sweeps from zero in one block (x in LDS, each
-// thread's cell coefficients in registers: a sweep touches no global memory);
+// thread's cell coefficients in registers: a sweep touches no global memory), up to MG_CPT cells
+// per thread (MG_COARSE > 1024: a coarsest level above 1024 cells, one V-cycle level less);
 // RZ (single-level hierarchy): also the partial f . x -> rz_part[0]
+constexpr int MG_CPT = (MG_COARSE + 1023) / 1024;
 template <bool RZ>
 __global__ __launch_bounds__(1024) void k_mg_coarse(MGLev L, const CGScal* S, const double* __restrict__ f,
                                                      double* __restrict__ xout, double* rz_part) {
     if (S->done) return;
     __shared__ double xs[2][3 * MG_COARSE];
     __shared__ double red[16];
-    const int n = L.w * L.h, i = threadIdx.x;
-    const bool in = i < n;
-    const int y = in ? i / L.w : 0, xx = in ? i - y * L.w : 0;
-    double f0 = 0, f1 = 0, f2v = 0;
-    double b[6] = {0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
-    const bool hxm = xx > 0, hxp = xx < L.w - 1, hym = y > 0, hyp = y < L.h - 1;
-    const double c = (double)mg_ncount(xx, y, L.w, L.h);
-    if (in) {
-        f0 = f[i]; f1 = f[n + i]; f2v = f[2 * n + i];
+    const int n = L.w * L.h;
+    double f0[MG_CPT], f1[MG_CPT], f2v[MG_CPT], b[MG_CPT][6], d[MG_CPT][6], c[MG_CPT];
+    int ci[MG_CPT];
+    bool in[MG_CPT], hxm[MG_CPT], hxp[MG_CPT], hym[MG_CPT], hyp[MG_CPT];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) { b[k] = L.B[k * n + i]; d[k] = L.Dinv[k * n + i]; }
-        const double z0 = d[0] * f0 + d[1] * f1 + d[2] * f2v, z1 = d[1] * f0 + d[3] * f1 + d[4] * f2v,
-                     z2 = d[2] * f0 + d[4] * f1 + d[5] * f2v;
-        xs[0][i] = MG_OMEGA * z0; xs[0][n + i] = MG_OMEGA * z1; xs[0][2 * n + i] = MG_OMEGA * z2;
+    for (int q = 0; q < MG_CPT; ++q) {
+        const int i = threadIdx.x + q * (int)blockDim.x;
+        ci[q] = i;
+        in[q] = i < n;
+        const int y = in[q] ? i / L.w : 0, xx = in[q] ? i - y * L.w : 0;
+        hxm[q] = xx > 0; hxp[q] = xx < L.w - 1; hym[q] = y > 0; hyp[q] = y < L.h - 1;
+        c[q] = (double)mg_ncount(xx, y, L.w, L.h);
+        f0[q] = f1[q] = f2v[q] = 0.0;
+        for (int k = 0; k < 6; ++k) { b[q][k] = 0.0; d[q][k] = 0.0; }
+        if (in[q]) {
+            f0[q] = f[i]; f1[q] = f[n + i]; f2v[q] = f[2 * n + i];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) { b[q][k] = L.B[k * n + i]; d[q][k] = L.Dinv[k * n + i]; }
+            const double z0 = d[q][0] * f0[q] + d[q][1] * f1[q] + d[q][2] * f2v[q],
+                         z1 = d[q][1] * f0[q] + d[q][3] * f1[q] + d[q][4] * f2v[q],
+                         z2 = d[q][2] * f0[q] + d[q][4] * f1[q] + d[q][5] * f2v[q];
+            xs[0][i] = MG_OMEGA * z0; xs[0][n + i] = MG_OMEGA * z1; xs[0][2 * n + i] = MG_OMEGA * z2;
+        }
     }
     __syncthreads();
     const double sc[3] = {L.s0, L.s1, L.s2};
     int cur = 0;
     for (int sweep = 1; sweep < MG_CSWEEPS; ++sweep) {
-        if (in) {
+#pragma unroll
+        for (int q = 0; q < MG_CPT; ++q) {
+            if (!in[q]) continue;
+            const int i = ci[q];
             const double* xc = xs[cur];
             double v[3], a[3];
 #pragma unroll
             for (int fl = 0; fl < 3; ++fl) {
-                const double* q = xc + fl * n;
-                v[fl] = q[i];
-                const double nb = (hxm ? q[i - 1] : 0.0) + (hxp ? q[i + 1] : 0.0) + (hym ? q[i - L.w] : 0.0) +
-                                  (hyp ? q[i + L.w] : 0.0);
-                a[fl] = sc[fl] * (c * v[fl] - nb);
+                const double* qq = xc + fl * n;
+                v[fl] = qq[i];
+                const double nb = (hxm[q] ? qq[i - 1] : 0.0) + (hxp[q] ? qq[i + 1] : 0.0) +
+                                  (hym[q] ? qq[i - L.w] : 0.0) + (hyp[q] ? qq[i + L.w] : 0.0);
+                a[fl] = sc[fl] * (c[q] * v[fl] - nb);
             }
-            const double r0 = f0 - (a[0] + b[0] * v[0] + b[1] * v[1] + b[2] * v[2]);
-            const double r1 = f1 - (a[1] + b[1] * v[0] + b[3] * v[1] + b[4] * v[2]);
-            const double r2 = f2v - (a[2] + b[2] * v[0] + b[4] * v[1] + b[5] * v[2]);
-            xs[cur ^ 1][i] = v[0] + MG_OMEGA * (d[0] * r0 + d[1] * r1 + d[2] * r2);
-            xs[cur ^ 1][n + i] = v[1] + MG_OMEGA * (d[1] * r0 + d[3] * r1 + d[4] * r2);
-            xs[cur ^ 1][2 * n + i] = v[2] + MG_OMEGA * (d[2] * r0 + d[4] * r1 + d[5] * r2);
+            const double r0 = f0[q] - (a[0] + b[q][0] * v[0] + b[q][1] * v[1] + b[q][2] * v[2]);
+            const double r1 = f1[q] - (a[1] + b[q][1] * v[0] + b[q][3] * v[1] + b[q][4] * v[2]);
+            const double r2 = f2v[q] - (a[2] + b[q][2] * v[0] + b[q][4] * v[1] + b[q][5] * v[2]);
+            xs[cur ^ 1][i] = v[0] + MG_OMEGA * (d[q][0] * r0 + d[q][1] * r1 + d[q][2] * r2);
+            xs[cur ^ 1][n + i] = v[1] + MG_OMEGA * (d[q][1] * r0 + d[q][3] * r1 + d[q][4] * r2);
+            xs[cur ^ 1][2 * n + i] = v[2] + MG_OMEGA * (d[q][2] * r0 + d[q][4] * r1 + d[q][5] * r2);
         }
         cur ^= 1;
         __syncthreads();
     }
     double rz = 0.0;
-    if (in) {
+#pragma unroll
+    for (int q = 0; q < MG_CPT; ++q) {
+        if (!in[q]) continue;
+        const int i = ci[q];
         xout[i] = xs[cur][i]; xout[n + i] = xs[cur][n + i]; xout[2 * n + i] = xs[cur][2 * n + i];
-        rz = f0 * xs[cur][i] + f1 * xs[cur][n + i] + f2v * xs[cur][2 * n + i];
+        rz += f0[q] * xs[cur][i] + f1[q] * xs[cur][n + i] + f2v[q] * xs[cur][2 * n + i];
     }
     if constexpr (RZ) {
         rz = gn_wave_sum(rz);
@@ -1040,6 +1248,8 @@ struct foto_gn_plan {
     double *d1 = nullptr, *d2 = nullptr, *fx = nullptr, *fy = nullptr, *ft = nullptr, *b = nullptr, *x = nullptr,
            *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr;
     double *rr_part = nullptr, *pq_part = nullptr, *rz_part[2] = {nullptr, nullptr};
+    double *r2 = nullptr, *q = nullptr, *rr_part2 = nullptr;   // the folded update (fold)
+    bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
     CGScal* hS = nullptr;
@@ -1081,11 +1291,12 @@ namespace foto {
 // between the sweeps)
 static int mg_coarse_threads(const foto_gn_plan::Lev& L) {
     const int n = L.w * L.h;
-    return std::min(1024, ((n + 63) / 64) * 64);
+    const int per = (n + MG_CPT - 1) / MG_CPT;   // (MG_COARSE <= 1024: one cell per thread)
+    return std::min(1024, ((per + 63) / 64) * 64);
 }
 
 // z = V(r) and the partials of r.z -> rz_out
-static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out) {
+static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out, const MGUpd* upd = nullptr) {
     hipStream_t s = P->s;
     const size_t nl = P->lev.size();
     if (nl == 1) {
@@ -1103,7 +1314,11 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
     for (size_t l = 0; l < ldown; ++l) {
         const auto& L = P->lev[l];
         const auto& C = P->lev[l + 1];
-        k_mg_down2<<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x, C.f);
+        if (l == 0 && upd)
+            k_mg_down2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, nullptr, L.x, C.f, *upd);
+        else
+            k_mg_down2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x,
+                                                               C.f, MGUpd{});
         FOTO_HIP_CHECK(hipGetLastError());
     }
     const size_t c = nl - 1;
@@ -1142,7 +1357,8 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
     return 0;
 }
 
-// PCG iteration of parity `par` (k even: p0 -> p1, z_k's r.z in rz_part[0])
+// PCG iteration of parity `par` (k even: p0 -> p1, z_k's r.z in rz_part[0]; folded update: r in
+// r, then r2 -> r by parity too)
 static int gn_iteration(foto_gn_plan* P, int par) {
     const int w = P->w, h = P->h;
     double* po = par ? P->p1 : P->p0;
@@ -1150,8 +1366,15 @@ static int gn_iteration(foto_gn_plan* P, int par) {
     const double* rzc = P->rz_part[par];
     const double* rzp = P->rz_part[par ^ 1];
     k_gnp_dir<<<P->nb_pix, NT, 0, P->s>>>(w, h, P->fx, P->fy, P->d2, P->alpha, P->lam, P->z, po, pn, P->dS,
-                                           P->rr_part, P->nb_pix, rzc, rzp, P->nb_rz, P->pq_part, P->rtol);
+                                           P->rr_part, P->nb_pix, rzc, rzp, P->nb_rz, P->pq_part, P->rtol,
+                                           P->fold ? P->q : nullptr, P->fold ? P->rr_part2 : nullptr, P->nb_rz);
     FOTO_HIP_CHECK(hipGetLastError());
+    if (P->fold) {
+        double* rold = par ? P->r2 : P->r;
+        double* rnew = par ? P->r : P->r2;
+        const MGUpd U{rold, rnew, P->q, pn, P->x, rzc, P->pq_part, P->rr_part2, P->dS, P->nb_rz, P->nb_pix};
+        return gn_vcycle(P, rnew, P->z, P->rz_part[par ^ 1], &U);
+    }
     k_gnp_upd<<<P->nb_pix, NT, 0, P->s>>>(w, h, P->fx, P->fy, P->d2, P->alpha, P->lam, pn, P->x, P->r, P->dS, rzc,
                                            P->nb_rz, P->pq_part, P->nb_pix, P->rr_part);
     FOTO_HIP_CHECK(hipGetLastError());
@@ -1185,7 +1408,7 @@ static int gn_plan_init(foto_gn_plan* P) {
     P->nb_pix = flat_blocks((int64_t)n);
     {
         const char* e = getenv("FOTO_MG_TAIL");
-        P->tail = e && atoi(e) != 0;
+        P->tail = e && atoi(e) != 0 && MG_COARSE <= 1024;   // (k_mg_tail: one coarsest cell per thread)
     }
     // level geometry
     int lw = w, lh = h;
@@ -1203,8 +1426,13 @@ static int gn_plan_init(foto_gn_plan* P) {
         sc *= 0.25;
     }
     P->nb_rz = P->lev.size() == 1 ? 1 : mg_tiles(w, h);
+    {
+        const char* e = getenv("FOTO_GN_FOLD");
+        P->fold = P->lev.size() > 1 && !(e && atoi(e) == 0);   // (one level: no down leg to fold into)
+    }
     const size_t nscal = sizeof(CGScal) / sizeof(double) + 1;
-    const size_t total = 23 * n + lev_total + 2 * (size_t)P->nb_pix + 2 * (size_t)P->nb_rz + nscal + 64;
+    const size_t nfold = P->fold ? 6 * n + (size_t)P->nb_rz : 0;
+    const size_t total = 23 * n + lev_total + 2 * (size_t)P->nb_pix + 2 * (size_t)P->nb_rz + nfold + nscal + 64;
     FOTO_HIP_CHECK(hipMalloc((void**)&P->base, total * sizeof(double)));
     tr.mark("device buffers");
     double* q = P->base;
@@ -1219,6 +1447,11 @@ static int gn_plan_init(foto_gn_plan* P) {
     P->pq_part = q; q += P->nb_pix;
     P->rz_part[0] = q; q += P->nb_rz;
     P->rz_part[1] = q; q += P->nb_rz;
+    if (P->fold) {
+        P->r2 = q; q += 3 * n;
+        P->q = q; q += 3 * n;
+        P->rr_part2 = q; q += P->nb_rz;
+    }
     P->dS = (CGScal*)q;
     // two iterations (p0 -> p1 -> p0) captured once; the kernels read the iteration index from
     // the device, so the graph is replayed unchanged
