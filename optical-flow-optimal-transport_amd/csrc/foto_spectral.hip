@@ -3191,6 +3191,7 @@ struct SpecImpl {
     GqNodes* gqn = nullptr;
     double* gq_hist = nullptr;    // world histograms (slot rank is this box's)
     bool gq_nodes_wave = true;    // k_gq_nodes_w (FOTO_GQ_NODES=thread: k_gq_nodes, the round-4 form)
+    bool gq_tfuse = false;        // x^ inside the inverse t-DCT (k_dct_t_inv_gq; FOTO_GQ_TFUSE)
     double* gq_tab = nullptr;
     GqBins* gq_bins = nullptr;    // bin edges of the measure and the solution table
     GqQCos* gq_qcos = nullptr;    // the solution table's transform constants
@@ -3433,6 +3434,8 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         FOTO_TRY(P->alloc(sizeof(double) * GQ_HIST * world, &b)); P->gq_hist = (double*)b;
         const char* gn = getenv("FOTO_GQ_NODES");
         P->gq_nodes_wave = !(gn && std::strcmp(gn, "thread") == 0);
+        const char* tf = getenv("FOTO_GQ_TFUSE");
+        P->gq_tfuse = tf && atoi(tf) != 0;
         FOTO_TRY(P->alloc(GQ_TAB_BYTES, &b)); P->gq_tab = (double*)b;
         // k_gq_xhat holds the whole table (128 KB) in dynamic LDS, beside its 10 KB bin tables
         FOTO_HIP_CHECK(hipFuncSetAttribute((const void*)k_gq_xhat, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3780,9 +3783,28 @@ static hipError_t launch_tcol(SpecImpl* P, bool inv, const double* in, double* o
     const SpecTab T = P->tab();
     const int nb = P->tcol_nb;
     const bool gq = inv && P->gauss_active;
-    if (gq) {   // x^ -> rh, then the plain inverse below
+    // one thread per column with the table in LDS: x^ = Q(lam) b^ inside the inverse t-DCT
+    bool tfuse = false;
+#define FOTO_TFUSE_NT(NN) tfuse = tfuse || P->g.Nt == NN;
+    FOTO_TCOL_SIZES(FOTO_TFUSE_NT)   // (one thread per column: Nt <= 32)
+#undef FOTO_TFUSE_NT
+    tfuse = tfuse && gq && P->gq_tfuse;
+    if (gq && !tfuse) {   // x^ -> rh, then the plain inverse below
         const hipError_t e = gq_xhat(P, P->rh, s);
         if (e != hipSuccess) return e;
+    }
+    if (tfuse) {
+        const int ql = 17;   // 2 blocks of 512 per CU (<= 80 KB of LDS each); rows beyond from the global table
+        const int nbf = (int)(((int64_t)P->nyl * P->g.Nx + GQ_TFNTH - 1) / GQ_TFNTH);
+#define FOTO_TFUSE_LAUNCH(NN)                                                                                      \
+        if (P->g.Nt == NN) {                                                                                       \
+            k_dct_t_inv_gq<NN><<<nbf, GQ_TFNTH, (size_t)ql * GQ_QB * sizeof(double), s>>>(                         \
+                    T, P->Cth, P->bh, P->gq_tab, P->gq, P->gq_bins, 1.0 / P->c1, out, ql);                       \
+            return hipGetLastError();                                                                              \
+        }
+        FOTO_TCOL_SIZES(FOTO_TFUSE_LAUNCH)
+#undef FOTO_TFUSE_LAUNCH
+        return hipErrorNotSupported;
     }
 #define FOTO_TCOL_FWD(NN, K, M) K<NN, M><<<nb, TC_NTH, 0, s>>>(T, P->Cth, in, P->bh, P->S2, P->rb, rtol, maxiter, \
                                                                 P->gath, P->rank)

@@ -141,3 +141,22 @@ def test_dct_xt_fused_opt_in(gold, monkeypatch, name):
     assert np.array_equal(k0, k1)
     np.testing.assert_allclose(c1, c0, rtol=1e-9, atol=0)
     np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-8 * np.abs(p0).max())
+
+
+@pytest.mark.parametrize("Nt,Nx,Ny", [(8, 64, 48), (32, 640, 480), (12, 50, 34)])
+def test_gq_tfuse_bit_identical(monkeypatch, Nt, Nx, Ny):
+    """FOTO_GQ_TFUSE=1: x^ = Q(lam) b^ inside the inverse t-DCT column kernel (k_dct_t_inv_gq)
+    instead of k_gq_xhat + the plain inverse: the same per-element arithmetic in the same order
+    (x^ and the DCT's half sums), so CG counts, crit and phi are bit-identical."""
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    out = {}
+    for tf in ("0", "1"):
+        monkeypatch.setenv("FOTO_GQ_TFUSE", tf)
+        with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=1.0, reg_epsilon=1e-2, cg_mode=3) as s:
+            s.iterate(4, 0.0, stop_rules=False)
+            out[tf] = (np.array(s.cg_its), np.array(s.crit), s.phi())
+    monkeypatch.delenv("FOTO_GQ_TFUSE")
+    (k0, c0, p0), (k1, c1, p1) = out["0"], out["1"]
+    assert np.array_equal(k0, k1)
+    assert np.array_equal(c0, c1)
+    assert np.array_equal(p0, p1)
