@@ -1234,6 +1234,269 @@ __global__ __launch_bounds__(1024) void k_mg_tail(MGTail T, const CGScal* S) {
     }
 }
 
+// ----------------------------------------------------------------------------- persistent small levels
+// The levels from l0 down (each at most MG_PT_TILES tiles), the coarsest solve and the up legs
+// back to l0 in ONE launch of tiles(l0) blocks (round 5, opt-in FOTO_MG_PTAIL=1): every small
+// level kernel sat at a ~5.5 us launch floor.  Measured slower (profiles/r05_gn_ptail.txt): at
+// 640x480 the launch takes 55 us for the 7 stages that the level kernels run in 43 -- a stage
+// here is ~8 us, its `sc1` loads of the previous stage's tiles (dropped from the L2 by the `sc1`
+// stores, served across the XCDs) plus the barrier cost as much as a kernel boundary does; the
+// polls' s_sleep is not it (the same without).  Stage s's blocks hand their tiles to
+// stage s + 1's through a grid barrier: every wave waits for its stores, the block joins a
+// workgroup barrier, one lane adds to an agent-scope arrival counter and polls it with `sc1`
+// loads until the whole grid has arrived.  Every load and store of the handed-off level arrays
+// (f, x, y) is an `sc1` access (agent-scope relaxed atomics: L2-served, coherent across the
+// XCDs without cache flushes -- MI355X_MICROARCH.md's hand-off table, row 1); B and D^-1 are
+// read-only here.  Each cell's arithmetic is the level kernels' in their order (the same
+// preconditioner bit for bit).  The counter only grows: launch i of a solve waits for
+// (i * syncs + s + 1) * blocks arrivals (i = the PCG iteration index, S->pad[0]); the host zeroes
+// it with the solve's scalars.  A poll that never completes (blocks not co-resident -- 64 small
+// blocks on a 256-CU device) gives up after ~1 s and flags S->pad[1] instead of hanging.
+#ifndef FOTO_PT_SLEEP
+#define FOTO_PT_SLEEP 2   // s_sleep between two polls of the arrival counter (A/B builds)
+#endif
+constexpr int MG_PT_TILES = 64;     // a level joins the tail when it has at most this many tiles
+constexpr int MG_PT_MAX = 8;
+struct MGPTail {
+    int nl;                         // levels l0 .. c (the last is the coarsest)
+    MGLev L[MG_PT_MAX];
+    double* f[MG_PT_MAX];
+    double* x[MG_PT_MAX];
+    double* y[MG_PT_MAX];
+    unsigned* counter;
+    int syncs;                      // grid barriers per launch
+};
+
+__device__ __forceinline__ double pt_ld(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pt_st(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void pt_grid_sync(unsigned* counter, unsigned target, CGScal* S) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int spins = 0;
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+#if FOTO_PT_SLEEP
+            __builtin_amdgcn_s_sleep(FOTO_PT_SLEEP);
+#endif
+            if (++spins > (1 << 20)) {   // (~1 s: a barrier normally completes in microseconds)   // never co-resident: flag it, do not hang the device
+                __hip_atomic_store(&S->pad[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void k_mg_ptail(MGPTail T, CGScal* S) {
+    if (S->done) return;
+    constexpr int XW = GT_X + 4, XH = GT_Y + 4, RW = GT_X + 2, RH = GT_Y + 2;
+    // one LDS pool: the level stages' x / r tiles, or the coarsest solve's two 3n buffers
+    constexpr int PT_POOL = (3 * XH * XW + 3 * RH * RW) > 6 * MG_COARSE ? (3 * XH * XW + 3 * RH * RW) : 6 * MG_COARSE;
+    __shared__ double pool[PT_POOL];
+    auto xs = reinterpret_cast<double(*)[XH][XW]>(pool);
+    auto rs = reinterpret_cast<double(*)[RH][RW]>(pool + 3 * XH * XW);
+    const unsigned nb = gridDim.x;
+    unsigned target = (unsigned)S->pad[0] * (unsigned)T.syncs * nb;
+    const int nl = T.nl, c = nl - 1;
+    // ---- down legs: k_mg_down2<false>'s three stages, tile = blockIdx.x
+    for (int l = 0; l < c; ++l) {
+        const MGLev L = T.L[l];
+        const int w = L.w, h = L.h, wc = T.L[l + 1].w, hc = T.L[l + 1].h;
+        const int tiles_x = (w + GT_X - 1) / GT_X, ntiles = tiles_x * ((h + GT_Y - 1) / GT_Y);
+        if ((int)blockIdx.x < ntiles) {
+            const int64_t n = (int64_t)w * h, nc = (int64_t)wc * hc;
+            const double* f = T.f[l];
+            double* xg = T.x[l];
+            double* fc = T.f[l + 1];
+            const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
+            for (int cc = threadIdx.x; cc < XH * XW; cc += NT) {
+                const int ly = cc / XW, lx = cc - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
+                double z0 = 0.0, z1 = 0.0, z2 = 0.0;
+                if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+                    const int64_t i = (int64_t)gy * w + gx;
+                    mg_dinv(L, i, pt_ld(&f[i]), pt_ld(&f[n + i]), pt_ld(&f[2 * n + i]), z0, z1, z2);
+                    z0 *= MG_OMEGA; z1 *= MG_OMEGA; z2 *= MG_OMEGA;
+                }
+                xs[0][ly][lx] = z0; xs[1][ly][lx] = z1; xs[2][ly][lx] = z2;
+            }
+            __syncthreads();
+            for (int cc = threadIdx.x; cc < RH * RW; cc += NT) {
+                const int ly = cc / RW, lx = cc - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+                double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+                if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+                    const int64_t i = (int64_t)gy * w + gx;
+                    double a0, a1, a2, v0, v1, v2;
+                    mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; },
+                               a0, a1, a2, v0, v1, v2);
+                    r0 = pt_ld(&f[i]) - a0; r1 = pt_ld(&f[n + i]) - a1; r2 = pt_ld(&f[2 * n + i]) - a2;
+                    if (ly >= 1 && ly <= GT_Y && lx >= 1 && lx <= GT_X) {
+                        pt_st(&xg[i], v0); pt_st(&xg[n + i], v1); pt_st(&xg[2 * n + i], v2);
+                    }
+                }
+                rs[0][ly][lx] = r0; rs[1][ly][lx] = r1; rs[2][ly][lx] = r2;
+            }
+            __syncthreads();
+            for (int cc = threadIdx.x; cc < (GT_Y / 2) * (GT_X / 2); cc += NT) {
+                const int cy = cc / (GT_X / 2), cx = cc - cy * (GT_X / 2);
+                const int J = y0 / 2 + cy, K = x0 / 2 + cx;
+                if (J >= hc || K >= wc) continue;
+                double wy[4], wx[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int y = 2 * J - 1 + d, x = 2 * K - 1 + d;
+                    wy[d] = (y >= 0 && y < h) ? mg_w1(y, J, hc) : 0.0;
+                    wx[d] = (x >= 0 && x < w) ? mg_w1(x, K, wc) : 0.0;
+                }
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+                for (int dy = 0; dy < 4; ++dy) {
+                    double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+#pragma unroll
+                    for (int dx = 0; dx < 4; ++dx) {
+                        const int ly = 2 * cy + dy, lx = 2 * cx + dx;
+                        b0 += wx[dx] * rs[0][ly][lx];
+                        b1 += wx[dx] * rs[1][ly][lx];
+                        b2 += wx[dx] * rs[2][ly][lx];
+                    }
+                    a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * b2;
+                }
+                const int64_t I = (int64_t)J * wc + K;
+                pt_st(&fc[I], 0.25 * a0);
+                pt_st(&fc[nc + I], 0.25 * a1);
+                pt_st(&fc[2 * nc + I], 0.25 * a2);
+            }
+        }
+        target += nb;
+        pt_grid_sync(T.counter, target, S);
+    }
+    // ---- the coarsest level: k_mg_coarse<false>'s sweeps in block 0, up to 4 cells per thread
+    if (blockIdx.x == 0) {
+        constexpr int CP = (MG_COARSE + NT - 1) / NT;
+        const MGLev L = T.L[c];
+        const int n = L.w * L.h;
+        auto xb = [&](int i) { return pool + i * (3 * MG_COARSE); };   // the two sweep buffers
+        const double* f = T.f[c];
+        double f0[CP], f1[CP], f2v[CP], b[CP][6], d[CP][6], cn[CP];
+        int ci[CP];
+        bool in[CP], hxm[CP], hxp[CP], hym[CP], hyp[CP];
+#pragma unroll
+        for (int q = 0; q < CP; ++q) {
+            const int i = threadIdx.x + q * NT;
+            ci[q] = i;
+            in[q] = i < n;
+            const int y = in[q] ? i / L.w : 0, xx = in[q] ? i - y * L.w : 0;
+            hxm[q] = xx > 0; hxp[q] = xx < L.w - 1; hym[q] = y > 0; hyp[q] = y < L.h - 1;
+            cn[q] = (double)mg_ncount(xx, y, L.w, L.h);
+            f0[q] = f1[q] = f2v[q] = 0.0;
+            for (int k = 0; k < 6; ++k) { b[q][k] = 0.0; d[q][k] = 0.0; }
+            if (in[q]) {
+                f0[q] = pt_ld(&f[i]); f1[q] = pt_ld(&f[n + i]); f2v[q] = pt_ld(&f[2 * n + i]);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) { b[q][k] = L.B[k * n + i]; d[q][k] = L.Dinv[k * n + i]; }
+                const double z0 = d[q][0] * f0[q] + d[q][1] * f1[q] + d[q][2] * f2v[q],
+                             z1 = d[q][1] * f0[q] + d[q][3] * f1[q] + d[q][4] * f2v[q],
+                             z2 = d[q][2] * f0[q] + d[q][4] * f1[q] + d[q][5] * f2v[q];
+                xb(0)[i] = MG_OMEGA * z0; xb(0)[n + i] = MG_OMEGA * z1; xb(0)[2 * n + i] = MG_OMEGA * z2;
+            }
+        }
+        __syncthreads();
+        const double sc[3] = {L.s0, L.s1, L.s2};
+        int cur = 0;
+        for (int sweep = 1; sweep < MG_CSWEEPS; ++sweep) {
+#pragma unroll
+            for (int q = 0; q < CP; ++q) {
+                if (!in[q]) continue;
+                const int i = ci[q];
+                const double* xc = xb(cur);
+                double v[3], a[3];
+#pragma unroll
+                for (int fl = 0; fl < 3; ++fl) {
+                    const double* qq = xc + fl * n;
+                    v[fl] = qq[i];
+                    const double nbv = (hxm[q] ? qq[i - 1] : 0.0) + (hxp[q] ? qq[i + 1] : 0.0) +
+                                       (hym[q] ? qq[i - L.w] : 0.0) + (hyp[q] ? qq[i + L.w] : 0.0);
+                    a[fl] = sc[fl] * (cn[q] * v[fl] - nbv);
+                }
+                const double r0 = f0[q] - (a[0] + b[q][0] * v[0] + b[q][1] * v[1] + b[q][2] * v[2]);
+                const double r1 = f1[q] - (a[1] + b[q][1] * v[0] + b[q][3] * v[1] + b[q][4] * v[2]);
+                const double r2 = f2v[q] - (a[2] + b[q][2] * v[0] + b[q][4] * v[1] + b[q][5] * v[2]);
+                xb(cur ^ 1)[i] = v[0] + MG_OMEGA * (d[q][0] * r0 + d[q][1] * r1 + d[q][2] * r2);
+                xb(cur ^ 1)[n + i] = v[1] + MG_OMEGA * (d[q][1] * r0 + d[q][3] * r1 + d[q][4] * r2);
+                xb(cur ^ 1)[2 * n + i] = v[2] + MG_OMEGA * (d[q][2] * r0 + d[q][4] * r1 + d[q][5] * r2);
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+        double* xo = T.x[c];
+#pragma unroll
+        for (int q = 0; q < CP; ++q) {
+            if (!in[q]) continue;
+            const int i = ci[q];
+            pt_st(&xo[i], xb(cur)[i]); pt_st(&xo[n + i], xb(cur)[n + i]); pt_st(&xo[2 * n + i], xb(cur)[2 * n + i]);
+        }
+    }
+    target += nb;
+    pt_grid_sync(T.counter, target, S);
+    // ---- up legs: k_mg_up2<false>'s two stages
+    for (int l = c - 1; l >= 0; --l) {
+        const MGLev L = T.L[l];
+        const int w = L.w, h = L.h, wc = T.L[l + 1].w, hc = T.L[l + 1].h;
+        const int tiles_x = (w + GT_X - 1) / GT_X, ntiles = tiles_x * ((h + GT_Y - 1) / GT_Y);
+        if ((int)blockIdx.x < ntiles) {
+            const int64_t n = (int64_t)w * h, nc = (int64_t)wc * hc;
+            const double* ec = (l + 1 == c) ? T.x[c] : T.y[l + 1];
+            const double* f = T.f[l];
+            const double* xg = T.x[l];
+            double* outp = T.y[l];
+            const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
+            for (int cc = threadIdx.x; cc < RH * RW; cc += NT) {
+                const int ly = cc / RW, lx = cc - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+                double v[3] = {0.0, 0.0, 0.0};
+                if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
+                    const int64_t i = (int64_t)gy * w + gx;
+                    const int X0 = gx >> 1, Y0 = gy >> 1;
+                    int X1 = (gx & 1) ? X0 + 1 : X0 - 1, Y1 = (gy & 1) ? Y0 + 1 : Y0 - 1;
+                    X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
+                    Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
+                    const int64_t c00 = (int64_t)Y0 * wc + X0, c01 = (int64_t)Y0 * wc + X1,
+                                  c10 = (int64_t)Y1 * wc + X0, c11 = (int64_t)Y1 * wc + X1;
+#pragma unroll
+                    for (int fl = 0; fl < 3; ++fl) {
+                        const double* e = ec + fl * nc;
+                        v[fl] = pt_ld(&xg[fl * n + i]) + (0.5625 * pt_ld(&e[c00]) + 0.1875 * pt_ld(&e[c01]) +
+                                                          0.1875 * pt_ld(&e[c10]) + 0.0625 * pt_ld(&e[c11]));
+                    }
+                }
+                xs[0][ly][lx] = v[0]; xs[1][ly][lx] = v[1]; xs[2][ly][lx] = v[2];
+            }
+            __syncthreads();
+            for (int cc = threadIdx.x; cc < GT_Y * GT_X; cc += NT) {
+                const int ly = cc / GT_X, lx = cc - ly * GT_X, gy = y0 + ly, gx = x0 + lx;
+                if (gx >= w || gy >= h) continue;
+                const int64_t i = (int64_t)gy * w + gx;
+                double a0, a1, a2, v0, v1, v2, z0, z1, z2;
+                mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0,
+                           a1, a2, v0, v1, v2);
+                const double f0 = pt_ld(&f[i]), f1 = pt_ld(&f[n + i]), f2v = pt_ld(&f[2 * n + i]);
+                mg_dinv(L, i, f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
+                pt_st(&outp[i], v0 + MG_OMEGA * z0);
+                pt_st(&outp[n + i], v1 + MG_OMEGA * z1);
+                pt_st(&outp[2 * n + i], v2 + MG_OMEGA * z2);
+            }
+        }
+        if (l > 0) {
+            target += nb;
+            pt_grid_sync(T.counter, target, S);
+        }
+    }
+}
+
 }  // namespace foto
 
 // ============================================================================ GN plan (host)
@@ -1250,6 +1513,8 @@ struct foto_gn_plan {
     double *rr_part = nullptr, *pq_part = nullptr, *rz_part[2] = {nullptr, nullptr};
     double *r2 = nullptr, *q = nullptr, *rr_part2 = nullptr;   // the folded update (fold)
     bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
+    size_t pt_l0 = 0;                // first level of the persistent small-level launch (0: none; FOTO_MG_PTAIL=1: on)
+    unsigned* pt_counter = nullptr;  // its grid-barrier arrivals (zeroed per solve)
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
     CGScal* hS = nullptr;
@@ -1310,6 +1575,7 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
         for (size_t l = 1; l < nl; ++l)
             if ((int64_t)P->lev[l].w * P->lev[l].h <= MG_TAIL_CELLS && nl - l <= (size_t)MG_TAIL_MAX) { l0 = l; break; }
     }
+    if (P->pt_l0 > 0) l0 = P->pt_l0;   // (the persistent launch replaces the one-block tail)
     const size_t ldown = std::min(l0, nl - 1);
     for (size_t l = 0; l < ldown; ++l) {
         const auto& L = P->lev[l];
@@ -1324,7 +1590,22 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
     const size_t c = nl - 1;
     const double* e = nullptr;
     size_t lup = nl - 1;   // up legs below this level run as level kernels
-    if (l0 < nl) {
+    if (P->pt_l0 > 0) {
+        MGPTail T{};
+        T.nl = (int)(nl - l0);
+        for (size_t l = l0; l < nl; ++l) {
+            T.L[l - l0] = P->desc(l);
+            T.f[l - l0] = P->lev[l].f;
+            T.x[l - l0] = P->lev[l].x;
+            T.y[l - l0] = P->lev[l].y;
+        }
+        T.counter = P->pt_counter;
+        T.syncs = 2 * (T.nl - 1);   // a barrier after each down leg, the coarsest solve, each up leg but the last
+        k_mg_ptail<<<mg_tiles(P->lev[l0].w, P->lev[l0].h), NT, 0, s>>>(T, P->dS);
+        FOTO_HIP_CHECK(hipGetLastError());
+        e = P->lev[l0].y;
+        lup = l0;
+    } else if (l0 < nl) {
         MGTail T{};
         T.nl = (int)(nl - l0);
         for (size_t l = l0; l < nl; ++l) {
@@ -1453,6 +1734,18 @@ static int gn_plan_init(foto_gn_plan* P) {
         P->rr_part2 = q; q += P->nb_rz;
     }
     P->dS = (CGScal*)q;
+    q += nscal;
+    P->pt_counter = (unsigned*)q;   // (within total's slack)
+    {   // the persistent small-level launch: from the first level of at most MG_PT_TILES tiles
+        const char* e = getenv("FOTO_MG_PTAIL");
+        const size_t nl = P->lev.size();
+        if (e && atoi(e) != 0 && !P->tail)   // (opt-in: measured slower, see k_mg_ptail)
+            for (size_t l = 1; l + 1 < nl; ++l)
+                if (mg_tiles(P->lev[l].w, P->lev[l].h) <= MG_PT_TILES) {
+                    if (nl - l <= (size_t)MG_PT_MAX) P->pt_l0 = l;
+                    break;
+                }
+    }
     // two iterations (p0 -> p1 -> p0) captured once; the kernels read the iteration index from
     // the device, so the graph is replayed unchanged
     FOTO_HIP_CHECK(hipStreamBeginCapture(P->s, hipStreamCaptureModeThreadLocal));
@@ -1496,6 +1789,7 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
         FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, f2, n * sizeof(double), hipMemcpyHostToDevice, s));
     }
     FOTO_HIP_CHECK(hipMemsetAsync(P->dS, 0, sizeof(CGScal), s));
+    if (P->pt_l0 > 0) FOTO_HIP_CHECK(hipMemsetAsync(P->pt_counter, 0, sizeof(unsigned), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->x, 0, 3 * n * sizeof(double), s));
     FOTO_HIP_CHECK(launch_gn_coeffs(w, h, P->d1, P->d2, P->fx, P->fy, P->ft, s));
     FOTO_HIP_CHECK(launch_gn_rhs(w, h, P->fx, P->fy, P->d2, P->ft, P->b, s));
@@ -1538,6 +1832,10 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     }
     FOTO_HIP_CHECK(hipEventRecord(P->ev[2], s));
     tr.mark("solve: PCG done");
+    if (P->hS->pad[1]) {   // (k_mg_ptail: a grid barrier gave up -- blocks not co-resident)
+        set_error("GN: the persistent small-level launch could not synchronise its blocks (FOTO_MG_PTAIL=0 avoids it)");
+        return FOTO_ERR_HIP;
+    }
     // the solution straight into the mapped pinned staging by a kernel: the first large
     // device-to-host hipMemcpy of a process took 8.5-14.8 ms at 640x480 (0.15-0.4 ms later)
     FOTO_TRY(gn_staging(P));   // (maxiter 0: no iteration ran)

@@ -637,6 +637,29 @@ def test_gn_solve_multilevel(pair, monkeypatch):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * max(1.0, np.abs(b).max()))
 
 
+@pytest.mark.parametrize("w,h", [(640, 480), (584, 388), (320, 240), (160, 120)])
+def test_gn_round5_forms_bit_identical(w, h, monkeypatch):
+    """Round 5's GN launch structures -- the PCG update folded into the level-0 down leg (the
+    default) and the small levels in one persistent launch with grid barriers (k_mg_ptail,
+    opt-in FOTO_MG_PTAIL=1) -- against the separate kernels (FOTO_GN_FOLD=0): every cell's
+    arithmetic is the same in the same order, so the iterates are bit-identical (only the stop
+    test's r.r is summed per tile), and the PCG counts match."""
+    from foto.synthetic import sinusoid_pair
+    f1, f2 = sinusoid_pair(w, h)
+    monkeypatch.setenv("FOTO_GN_PLAN_CACHE", "0")
+    out = {}
+    for key, fold, pt in (("sep", "0", "0"), ("fold", "1", "0"), ("ptail", "1", "1")):
+        monkeypatch.setenv("FOTO_GN_FOLD", fold)
+        monkeypatch.setenv("FOTO_MG_PTAIL", pt)
+        out[key] = gn.solve(f1, f2, w, h, 0.1, 0.2)
+    for key in ("fold", "ptail"):
+        u, v, m, info, its = out[key]
+        print(f"{w}x{h} {key}: {its} PCG its (separate kernels: {out['sep'][4]})")
+        assert info == 0 and its == out["sep"][4]
+        for a, b in zip((u, v, m), out["sep"][:3]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_gn_plan_reuse():
     """One gn.Plan (classical.GLLOpticalFlow after setAlpha/setLambda) solving pairs in turn:
     every solve equals the one-shot foto_gn_solve bit for bit (same kernels, same graph), the
