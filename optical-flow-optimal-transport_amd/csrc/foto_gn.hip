@@ -1497,6 +1497,189 @@ __global__ __launch_bounds__(NT) void k_mg_ptail(MGPTail T, CGScal* S) {
     }
 }
 
+// ----------------------------------------------------------------------------- last level + coarsest in LDS
+// The down leg of the level above the coarsest, the coarsest solve and that level's up leg in one
+// block whose vectors never leave the LDS (round 5, default where the level has at most
+// MG_LT_CELLS cells: 40x30 at 640x480 and 320x240; FOTO_MG_LTAIL=0: the three level kernels).
+// The one-block tail of round 3 kept its level arrays in global memory and was slower; here
+// f, x, r and the coarse vectors sit in ~94 KB of LDS, each cell's B and D^-1 in registers, and
+// the stages are separated by workgroup barriers only.  Every cell's arithmetic is the level
+// kernels' (k_mg_down2, k_mg_coarse, k_mg_up2) in their order: the same preconditioner bit for
+// bit.  Reads f of the level (the down leg above wrote it), writes only the up leg's output y.
+constexpr int MG_LT_CELLS = 1536;
+constexpr int MG_LT_NTH = 512;    // (1024 threads: 128 VGPRs, the cells' coefficients spilled)
+constexpr int MG_LT_CPT = (MG_LT_CELLS + MG_LT_NTH - 1) / MG_LT_NTH;   // fine cells per thread
+__host__ __device__ constexpr size_t mg_lt_lds(int n, int nc) {   // doubles of dynamic LDS
+    return 3 * (size_t)n + 3 * (size_t)n + (3 * (size_t)n > 6 * (size_t)nc ? 3 * (size_t)n : 6 * (size_t)nc) +
+           3 * (size_t)nc;
+}
+__global__ __launch_bounds__(MG_LT_NTH) void k_mg_ltail(MGLev L, MGLev C, const CGScal* S,
+                                                        const double* __restrict__ f, double* __restrict__ y) {
+    if (S->done) return;
+    extern __shared__ double lds[];
+    const int w = L.w, h = L.h, n = w * h, wc = C.w, hc = C.h, nc = wc * hc;
+    double* fL = lds;               // f of the level
+    double* xL = fL + 3 * n;        // the down leg's x, then x' = x + P e
+    double* rL = xL + 3 * n;        // r, then the coarse solve's two sweep buffers
+    double* fcL = rL + (3 * n > 6 * nc ? 3 * n : 6 * nc);   // f of the coarsest level
+    const int tid = threadIdx.x;
+    // the coarsest cell's coefficients first (they were a dependent round trip mid-kernel)
+    double cb[6], cd[6];
+    {
+        const bool cin = tid < nc;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            cb[k] = cin ? C.B[k * nc + tid] : 0.0;
+            cd[k] = cin ? C.Dinv[k * nc + tid] : 0.0;
+        }
+    }
+    // the fine cells' coefficients in registers; f into LDS
+    double bq[MG_LT_CPT][6], dq[MG_LT_CPT][6];
+#pragma unroll
+    for (int q = 0; q < MG_LT_CPT; ++q) {
+        const int i = tid + q * MG_LT_NTH;
+        if (i < n) {
+            for (int k = 0; k < 6; ++k) { bq[q][k] = L.B[k * n + i]; dq[q][k] = L.Dinv[k * n + i]; }
+            for (int fl = 0; fl < 3; ++fl) fL[fl * n + i] = f[fl * n + i];
+        } else {
+            for (int k = 0; k < 6; ++k) { bq[q][k] = 0.0; dq[q][k] = 0.0; }
+        }
+    }
+    __syncthreads();
+    // down leg, stage 1: x = omega D^-1 f
+#pragma unroll
+    for (int q = 0; q < MG_LT_CPT; ++q) {
+        const int i = tid + q * MG_LT_NTH;
+        if (i >= n) continue;
+        double z0, z1, z2;
+        mg_dinv_v(dq[q], fL[i], fL[n + i], fL[2 * n + i], z0, z1, z2);
+        xL[i] = z0 * MG_OMEGA; xL[n + i] = z1 * MG_OMEGA; xL[2 * n + i] = z2 * MG_OMEGA;
+    }
+    __syncthreads();
+    // stage 2: r = f - A x
+#pragma unroll
+    for (int q = 0; q < MG_LT_CPT; ++q) {
+        const int i = tid + q * MG_LT_NTH;
+        if (i >= n) continue;
+        const int gy = i / w, gx = i - gy * w;
+        double a0, a1, a2, v0, v1, v2;
+        mg_apply_b(L, gx, gy, bq[q], [&](int fl, int dy, int dx) { return xL[fl * n + i + dy * w + dx]; }, a0, a1,
+                   a2, v0, v1, v2);
+        rL[i] = fL[i] - a0; rL[n + i] = fL[n + i] - a1; rL[2 * n + i] = fL[2 * n + i] - a2;
+    }
+    __syncthreads();
+    // stage 3: fc = R r (4 x 4 taps; taps outside the grid weigh 0 and read 0, as the tile's halo)
+    for (int I0 = tid; I0 < nc; I0 += MG_LT_NTH) {
+        const int J = I0 / wc, K = I0 - J * wc;
+        double wy[4], wx[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int yy = 2 * J - 1 + d, xx = 2 * K - 1 + d;
+            wy[d] = (yy >= 0 && yy < h) ? mg_w1(yy, J, hc) : 0.0;
+            wx[d] = (xx >= 0 && xx < w) ? mg_w1(xx, K, wc) : 0.0;
+        }
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) {
+            double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+            const int yy = 2 * J - 1 + dy;
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx) {
+                const int xx = 2 * K - 1 + dx;
+                const bool in = yy >= 0 && yy < h && xx >= 0 && xx < w;
+                const int i = in ? yy * w + xx : 0;
+                b0 += wx[dx] * (in ? rL[i] : 0.0);
+                b1 += wx[dx] * (in ? rL[n + i] : 0.0);
+                b2 += wx[dx] * (in ? rL[2 * n + i] : 0.0);
+            }
+            a0 += wy[dy] * b0; a1 += wy[dy] * b1; a2 += wy[dy] * b2;
+        }
+        fcL[I0] = 0.25 * a0;
+        fcL[nc + I0] = 0.25 * a1;
+        fcL[2 * nc + I0] = 0.25 * a2;
+    }
+    __syncthreads();
+    // the coarsest level: k_mg_coarse<false>'s sweeps (one cell per thread: the host checks nc <= MG_LT_NTH)
+    {
+        double* xb0 = rL;
+        double* xb1 = rL + 3 * nc;
+        const int i = tid;
+        const bool in = i < nc;
+        const int yc = in ? i / wc : 0, xc = in ? i - yc * wc : 0;
+        double f0 = 0, f1 = 0, f2v = 0, b[6], d[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { b[k] = cb[k]; d[k] = cd[k]; }
+        const bool hxm = xc > 0, hxp = xc < wc - 1, hym = yc > 0, hyp = yc < hc - 1;
+        const double cn = (double)mg_ncount(xc, yc, wc, hc);
+        if (in) {
+            f0 = fcL[i]; f1 = fcL[nc + i]; f2v = fcL[2 * nc + i];
+            const double z0 = d[0] * f0 + d[1] * f1 + d[2] * f2v, z1 = d[1] * f0 + d[3] * f1 + d[4] * f2v,
+                         z2 = d[2] * f0 + d[4] * f1 + d[5] * f2v;
+            xb0[i] = MG_OMEGA * z0; xb0[nc + i] = MG_OMEGA * z1; xb0[2 * nc + i] = MG_OMEGA * z2;
+        }
+        __syncthreads();
+        const double sc[3] = {C.s0, C.s1, C.s2};
+        int cur = 0;
+        for (int sweep = 1; sweep < MG_CSWEEPS; ++sweep) {
+            if (in) {
+                const double* xcur = cur ? xb1 : xb0;
+                double* xnext = cur ? xb0 : xb1;
+                double v[3], a[3];
+#pragma unroll
+                for (int fl = 0; fl < 3; ++fl) {
+                    const double* qq = xcur + fl * nc;
+                    v[fl] = qq[i];
+                    const double nbv = (hxm ? qq[i - 1] : 0.0) + (hxp ? qq[i + 1] : 0.0) + (hym ? qq[i - wc] : 0.0) +
+                                       (hyp ? qq[i + wc] : 0.0);
+                    a[fl] = sc[fl] * (cn * v[fl] - nbv);
+                }
+                const double r0 = f0 - (a[0] + b[0] * v[0] + b[1] * v[1] + b[2] * v[2]);
+                const double r1 = f1 - (a[1] + b[1] * v[0] + b[3] * v[1] + b[4] * v[2]);
+                const double r2 = f2v - (a[2] + b[2] * v[0] + b[4] * v[1] + b[5] * v[2]);
+                xnext[i] = v[0] + MG_OMEGA * (d[0] * r0 + d[1] * r1 + d[2] * r2);
+                xnext[nc + i] = v[1] + MG_OMEGA * (d[1] * r0 + d[3] * r1 + d[4] * r2);
+                xnext[2 * nc + i] = v[2] + MG_OMEGA * (d[2] * r0 + d[4] * r1 + d[5] * r2);
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+        // up leg, stage 1: x' = x + P e (pointwise: in place)
+        const double* ec = cur ? xb1 : xb0;
+#pragma unroll
+        for (int q = 0; q < MG_LT_CPT; ++q) {
+            const int ii = tid + q * MG_LT_NTH;
+            if (ii >= n) continue;
+            const int gy = ii / w, gx = ii - gy * w;
+            const int X0 = gx >> 1, Y0 = gy >> 1;
+            int X1 = (gx & 1) ? X0 + 1 : X0 - 1, Y1 = (gy & 1) ? Y0 + 1 : Y0 - 1;
+            X1 = X1 < 0 ? 0 : (X1 > wc - 1 ? wc - 1 : X1);
+            Y1 = Y1 < 0 ? 0 : (Y1 > hc - 1 ? hc - 1 : Y1);
+            const int c00 = Y0 * wc + X0, c01 = Y0 * wc + X1, c10 = Y1 * wc + X0, c11 = Y1 * wc + X1;
+#pragma unroll
+            for (int fl = 0; fl < 3; ++fl) {
+                const double* e = ec + fl * nc;
+                xL[fl * n + ii] = xL[fl * n + ii] + (0.5625 * e[c00] + 0.1875 * e[c01] + 0.1875 * e[c10] + 0.0625 * e[c11]);
+            }
+        }
+    }
+    __syncthreads();
+    // stage 2: y = x' + omega D^-1 (f - A x')
+#pragma unroll
+    for (int q = 0; q < MG_LT_CPT; ++q) {
+        const int i = tid + q * MG_LT_NTH;
+        if (i >= n) continue;
+        const int gy = i / w, gx = i - gy * w;
+        double a0, a1, a2, v0, v1, v2, z0, z1, z2;
+        mg_apply_b(L, gx, gy, bq[q], [&](int fl, int dy, int dx) { return xL[fl * n + i + dy * w + dx]; }, a0, a1,
+                   a2, v0, v1, v2);
+        const double f0 = fL[i], f1 = fL[n + i], f2v = fL[2 * n + i];
+        mg_dinv_v(dq[q], f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
+        y[i] = v0 + MG_OMEGA * z0;
+        y[n + i] = v1 + MG_OMEGA * z1;
+        y[2 * n + i] = v2 + MG_OMEGA * z2;
+    }
+}
+
 }  // namespace foto
 
 // ============================================================================ GN plan (host)
@@ -1514,6 +1697,7 @@ struct foto_gn_plan {
     double *r2 = nullptr, *q = nullptr, *rr_part2 = nullptr;   // the folded update (fold)
     bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
     size_t pt_l0 = 0;                // first level of the persistent small-level launch (0: none; FOTO_MG_PTAIL=1: on)
+    bool lt = false;                 // the last level + coarsest in one LDS-resident block (k_mg_ltail)
     unsigned* pt_counter = nullptr;  // its grid-barrier arrivals (zeroed per solve)
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
@@ -1576,6 +1760,38 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
             if ((int64_t)P->lev[l].w * P->lev[l].h <= MG_TAIL_CELLS && nl - l <= (size_t)MG_TAIL_MAX) { l0 = l; break; }
     }
     if (P->pt_l0 > 0) l0 = P->pt_l0;   // (the persistent launch replaces the one-block tail)
+    if (P->lt) {   // level c - 1 and the coarsest in one block: the level kernels above and below it
+        const size_t c = nl - 1;
+        for (size_t l = 0; l + 1 < c; ++l) {
+            const auto& L = P->lev[l];
+            const auto& C = P->lev[l + 1];
+            if (l == 0 && upd)
+                k_mg_down2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, nullptr, L.x, C.f, *upd);
+            else
+                k_mg_down2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x,
+                                                                   C.f, MGUpd{});
+            FOTO_HIP_CHECK(hipGetLastError());
+        }
+        const auto& L = P->lev[c - 1];
+        const auto& C = P->lev[c];
+        k_mg_ltail<<<1, MG_LT_NTH, mg_lt_lds(L.w * L.h, C.w * C.h) * sizeof(double), s>>>(P->desc(c - 1), P->desc(c),
+                                                                                          P->dS, L.f, L.y);
+        FOTO_HIP_CHECK(hipGetLastError());
+        const double* e = L.y;
+        for (size_t l = c - 1; l-- > 0;) {
+            const auto& Lu = P->lev[l];
+            const auto& Cu = P->lev[l + 1];
+            if (l == 0) {
+                k_mg_up2<true><<<mg_tiles(Lu.w, Lu.h), NT, 0, s>>>(P->desc(0), Cu.w, Cu.h, P->dS, e, r, Lu.x, z, rz_out);
+            } else {
+                k_mg_up2<false><<<mg_tiles(Lu.w, Lu.h), NT, 0, s>>>(P->desc(l), Cu.w, Cu.h, P->dS, e, Lu.f, Lu.x, Lu.y,
+                                                                    nullptr);
+                e = Lu.y;
+            }
+            FOTO_HIP_CHECK(hipGetLastError());
+        }
+        return 0;
+    }
     const size_t ldown = std::min(l0, nl - 1);
     for (size_t l = 0; l < ldown; ++l) {
         const auto& L = P->lev[l];
@@ -1745,6 +1961,19 @@ static int gn_plan_init(foto_gn_plan* P) {
                     if (nl - l <= (size_t)MG_PT_MAX) P->pt_l0 = l;
                     break;
                 }
+    }
+    {   // the last level above the coarsest and the coarsest in LDS (FOTO_MG_LTAIL=0: level kernels)
+        const char* e = getenv("FOTO_MG_LTAIL");
+        const size_t nl = P->lev.size();
+        if (!(e && atoi(e) == 0) && !P->tail && P->pt_l0 == 0 && nl >= 3 &&
+            (int64_t)P->lev[nl - 2].w * P->lev[nl - 2].h <= MG_LT_CELLS &&
+            (int64_t)P->lev[nl - 1].w * P->lev[nl - 1].h <= MG_LT_NTH) {
+            P->lt = true;
+            const size_t bytes = mg_lt_lds(P->lev[nl - 2].w * P->lev[nl - 2].h, P->lev[nl - 1].w * P->lev[nl - 1].h) *
+                                 sizeof(double);
+            FOTO_HIP_CHECK(hipFuncSetAttribute((const void*)k_mg_ltail, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)bytes));
+        }
     }
     // two iterations (p0 -> p1 -> p0) captured once; the kernels read the iteration index from
     // the device, so the graph is replayed unchanged

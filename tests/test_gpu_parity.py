@@ -639,20 +639,23 @@ def test_gn_solve_multilevel(pair, monkeypatch):
 
 @pytest.mark.parametrize("w,h", [(640, 480), (584, 388), (320, 240), (160, 120)])
 def test_gn_round5_forms_bit_identical(w, h, monkeypatch):
-    """Round 5's GN launch structures -- the PCG update folded into the level-0 down leg (the
-    default) and the small levels in one persistent launch with grid barriers (k_mg_ptail,
-    opt-in FOTO_MG_PTAIL=1) -- against the separate kernels (FOTO_GN_FOLD=0): every cell's
+    """Round 5's GN launch structures -- the PCG update folded into the level-0 down leg and the
+    last level above the coarsest solved with it in one LDS-resident block (k_mg_ltail; both
+    default), the small levels in one persistent launch with grid barriers (k_mg_ptail, opt-in
+    FOTO_MG_PTAIL=1) -- against the separate kernels (FOTO_GN_FOLD=0 ...): every cell's
     arithmetic is the same in the same order, so the iterates are bit-identical (only the stop
     test's r.r is summed per tile), and the PCG counts match."""
     from foto.synthetic import sinusoid_pair
     f1, f2 = sinusoid_pair(w, h)
     monkeypatch.setenv("FOTO_GN_PLAN_CACHE", "0")
     out = {}
-    for key, fold, pt in (("sep", "0", "0"), ("fold", "1", "0"), ("ptail", "1", "1")):
+    forms = (("sep", "0", "0", "0"), ("fold", "1", "0", "0"), ("ltail", "1", "0", "1"), ("ptail", "1", "1", "0"))
+    for key, fold, pt, lt in forms:
         monkeypatch.setenv("FOTO_GN_FOLD", fold)
         monkeypatch.setenv("FOTO_MG_PTAIL", pt)
+        monkeypatch.setenv("FOTO_MG_LTAIL", lt)
         out[key] = gn.solve(f1, f2, w, h, 0.1, 0.2)
-    for key in ("fold", "ptail"):
+    for key in ("fold", "ltail", "ptail"):
         u, v, m, info, its = out[key]
         print(f"{w}x{h} {key}: {its} PCG its (separate kernels: {out['sep'][4]})")
         assert info == 0 and its == out["sep"][4]

@@ -19,6 +19,8 @@ timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/cal_write -o run -- t
 # kernel's launches of each segment (tools/prox_segments.py)
 rm -rf $O/prof_kt2
 timeout -k 10 240 rocprofv3 --kernel-trace -f csv -d $O/prof_kt2 -o run -- python3 bench.py $args > $O/prof_kt2.log 2>&1 || exit $?
-python3 tools/prox_segments.py $O/prof_kt2/run_kernel_trace.csv 10 2 > $O/prox_segments.txt || exit $?
+python3 tools/prox_segments.py $O/prof_kt2/run_kernel_trace.csv 10 2 $O/prox_loop_trace.json \
+    "profiles/${tag}_prox_segments.txt (rocprofv3 --kernel-trace of bench.py $args: k_prox_rhs in the timed loop vs in the HIP-event timing pass, same run)" \
+    > $O/prox_segments.txt || exit $?
 python3 tools/summarize_profile.py --tag "$tag" --kt $O/prof_kt --fetch $O/prof_fetch --write $O/prof_write \
     --calib-fetch $O/cal_fetch --calib-write $O/cal_write --bench $O/bench_full.log --out $O/profiles_new
