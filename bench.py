@@ -66,6 +66,7 @@ def parse():
                     help="N > 1: batch = one solve per GPU (weak scaling, default); sharded = one solve time-sharded "
                          "over the N GPUs (strong scaling)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1, batch mode: skip the time-sharded side run")
+    ap.add_argument("--strong-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -108,11 +109,11 @@ class FileRendezvous:
     keyed by MASTER_PORT and the launcher's pid (every rank is a child of the same
     torch.distributed.run agent), files for the RCCL unique id, barriers and per-rank times."""
 
-    def __init__(self, rank, world, timeout=300.0):
+    def __init__(self, rank, world, timeout=300.0, dir=None):
         import tempfile
         self.rank, self.world, self.timeout, self.n = rank, world, timeout, 0
         key = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
-        self.dir = os.path.join(tempfile.gettempdir(), f"foto_bench_{key}")
+        self.dir = dir or os.path.join(tempfile.gettempdir(), f"foto_bench_{key}")
         os.makedirs(self.dir, exist_ok=True)
 
     def _wait(self, paths):
@@ -373,50 +374,69 @@ def survey_bytes(k):
     return (21 + 10 * k) * NX * NY * NT * 8
 
 
-def strong_side(args, rdv, rank, world, local_rank, nccl_id, rho0, rhoT):
+def strong_side(args, rdv, rank, world, local_rank):
     """Batch mode, N > 1: ONE solve time-sharded over the N GPUs (config 4's decomposition over
-    RCCL) on the same workload: warmup, barrier, K timed outer iterations, the slowest rank's
-    clock.  A watchdog ends the process after FOTO_BENCH_STRONG_TIMEOUT s (default 180) with the
-    headline line printed by rank 0 and "strong": {"error": "timeout"} -- a collective that
-    never completes cannot cost the data-parallel measurement."""
-    import threading
-    from foto.bb import BBSolver
+    RCCL) on the same workload, run by a child process per rank (`--strong-child`): warmup,
+    barrier, K timed outer iterations, the slowest rank's clock.  Each rank waits for its child
+    at most FOTO_BENCH_STRONG_TIMEOUT s (default 180) and kills it after that -- a collective that
+    never completes, or a crash inside RCCL, cannot cost the data-parallel headline, which this
+    process prints either way (the RCCL calls have run only through the in-process transport
+    before, never across GPUs)."""
+    import subprocess
     limit = float(os.environ.get("FOTO_BENCH_STRONG_TIMEOUT", "180"))
-    done = threading.Event()
-
-    def watchdog():
-        if not done.wait(limit):
-            if rank == 0 and _PENDING_LINE:
-                _PENDING_LINE[0]["strong"] = {"error": f"timeout after {limit:.0f} s"}
-                print(json.dumps(_PENDING_LINE[0]), flush=True)
-            os._exit(0)
-
-    threading.Thread(target=watchdog, daemon=True).start()
+    env = dict(os.environ, FOTO_BENCH_RDV_DIR=os.path.join(rdv.dir, "strong"), FOTO_BENCH_PARENT_RDV=rdv.dir,
+               FOTO_BENCH_LOCAL_DEVICE=str(local_rank))
+    cmd = [sys.executable, os.path.abspath(__file__), "--strong-child", "--gpus", str(world), "--steps",
+           str(args.steps), "--warmup", str(args.warmup), "--cg-mode", str(args.cg_mode)]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
-        with BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=local_rank, cg_mode=args.cg_mode,
-                      rank=rank, world=world, nccl_id=nccl_id) as t:
-            t.iterate(args.warmup, 0.0, stop_rules=False)
-            t.sync()
-            rdv.barrier()
-            n0 = len(t.cg_its)
-            t0 = time.perf_counter()
-            t.iterate(args.steps, 0.0, stop_rules=False)
-            t.sync()
-            el = rdv.max(time.perf_counter() - t0)
-            rdv.barrier()
-            cg = t.cg_its[n0:]
-        out = {"value": round(args.steps / el, 4), "unit": "iters/s", "ms_per_step": round(1e3 * el / args.steps, 3),
-               "steps": args.steps, "scaling": "strong", "n_gpus": world,
-               "cg_iters_per_step": round(float(np.mean(cg)), 2) if cg else None,
-               "parallelism": f"time-slab x{world}: {NT} planes split over {world} ranks, slab <-> row-box all-to-alls "
-                              f"(pipelined, phi's halo inside) and the w_t halo over RCCL (DESIGN.md 5)"}
-    except Exception as e:   # reported, not fatal: the headline is the data-parallel run
-        out = {"error": f"{type(e).__name__}: {e}"[:300]}
-    done.set()
-    return out
+        out, err = proc.communicate(timeout=limit)
+    except subprocess.TimeoutExpired:
+        proc.kill()   # (this rank's own child, by its handle)
+        proc.communicate()
+        return {"error": f"timeout after {limit:.0f} s"}
+    if proc.returncode != 0:
+        tail = (err or "").strip().splitlines()[-3:]
+        return {"error": f"strong side run exited {proc.returncode}: {' | '.join(tail)}"[:300]}
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if rank != 0:
+        return None
+    return json.loads(lines[-1]) if lines else {"error": "no result line"}
 
 
-_PENDING_LINE = []   # rank 0's line while the strong side run is in flight (its watchdog prints it)
+def strong_child(args):
+    """The strong side run's worker (one per rank, started by strong_side): its own rendezvous
+    directory inside the parent's, the RCCL id rank 0's parent broadcast, the same workload."""
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    device = int(os.environ["FOTO_BENCH_LOCAL_DEVICE"])
+    rdv = FileRendezvous(rank, world, timeout=120, dir=os.environ["FOTO_BENCH_RDV_DIR"])
+    with open(os.path.join(os.environ["FOTO_BENCH_PARENT_RDV"], "nccl_id"), "rb") as f:
+        nccl_id = f.read()
+    from foto.bb import BBSolver
+    from foto.synthetic import translating_gaussian
+    rho0, rhoT = translating_gaussian(NX, NY)
+    with BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=device, cg_mode=args.cg_mode,
+                  rank=rank, world=world, nccl_id=nccl_id) as t:
+        t.iterate(args.warmup, 0.0, stop_rules=False)
+        t.sync()
+        rdv.barrier()
+        n0 = len(t.cg_its)
+        t0 = time.perf_counter()
+        t.iterate(args.steps, 0.0, stop_rules=False)
+        t.sync()
+        el = rdv.max(time.perf_counter() - t0)
+        rdv.barrier()
+        cg = t.cg_its[n0:]
+    rdv.close()
+    if rank == 0:
+        print(json.dumps({"value": round(args.steps / el, 4), "unit": "iters/s", "ms_per_step": round(1e3 * el / args.steps, 3),
+                          "steps": args.steps, "scaling": "strong", "n_gpus": world,
+                          "cg_iters_per_step": round(float(np.mean(cg)), 2) if cg else None,
+                          "parallelism": f"time-slab x{world}: {NT} planes split over {world} ranks, slab <-> row-box "
+                                         f"all-to-alls and the w_t halo over RCCL (DESIGN.md 5)"}), flush=True)
+
+
 
 
 def main():
@@ -426,6 +446,9 @@ def main():
         return
     if args.gn_cpu_only:
         gn_cpu_child()
+        return
+    if args.strong_child:
+        strong_child(args)
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -584,10 +607,8 @@ def main():
         if roof is not None:
             roof["step"] = step_roofline(args.cg_mode, world if sharded else 1, elapsed / args.steps)
     s.close()
-    if want_strong:   # (after the headline line exists: the side run's watchdog prints it on a timeout)
-        if line is not None:
-            _PENDING_LINE.append(line)
-        strong = strong_side(args, rdv, rank, world, local_rank, nccl_id, rho0, rhoT)
+    if want_strong:   # (child processes: a hang or crash in RCCL is reported, not fatal)
+        strong = strong_side(args, rdv, rank, world, local_rank)
         if line is not None:
             line["strong"] = strong
     if line is not None and world == 1 and args.cg_mode != 0 and not args.no_stencil:

@@ -72,3 +72,28 @@ def test_bench_two_ranks_batch_mode_one_gpu(tmp_path):
     assert abs(d["value"] * d["ms_per_step"] / 1e3 - 2.0) < 0.02
     assert 150 <= d["cg_iters_per_step"] <= 210
     assert "strong" not in d
+
+
+def test_bench_strong_side_run_failure_is_reported(tmp_path):
+    """The batch mode's time-sharded side run runs in a child process per rank: here, with both
+    ranks on one GPU, RCCL refuses the communicator (one device for two ranks), and the children
+    fail -- the headline line must still come out of rank 0 with the failure reported in
+    "strong", and both ranks must exit 0 (a crash or hang inside RCCL on the driver's 8-GPU node
+    cannot cost the data-parallel measurement)."""
+    procs = []
+    for g in range(2):
+        env = dict(os.environ, FOTO_BENCH_DEVICES="0,0", WORLD_SIZE="2", RANK=str(g), LOCAL_RANK=str(g),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT="29619", FOTO_BENCH_STRONG_TIMEOUT="90")
+        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline", "--no-gn", "--no-stencil"]
+        procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [ln for o, _ in outs for ln in o.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, [o[-1000:] for o, _ in outs]
+    d = json.loads(lines[0])
+    print("strong:", d.get("strong"))
+    assert d["scaling"] == "weak" and d["n_gpus"] == 2
+    assert "strong" in d and ("error" in d["strong"] or "value" in d["strong"])

@@ -100,6 +100,32 @@ def test_metric_grid_true_residual_ten_outer(mode):
     np.testing.assert_allclose(crit_one, crit_steps, rtol=1e-9, atol=0)
 
 
+def test_c5_runsh_params_middlebury2_size_vs_oracle():
+    """C5's per-sequence solve at run.sh's own parameters (r 1, reg-epsilon 1e-2, Nt 16) at a
+    Middlebury-2 size (Dimetrodon's 584x388) on a textured pair, against the oracle's restatement
+    of benamou_brenier.solve (tests only: oracle/foto_oracle.py, scipy CG on the assembled A)
+    for three outer iterations -- the metric grid's bars: CG counts +-1, crit 1e-8 relative, phi
+    1e-8 of max|phi|, flow 1e-7 px.  (run.sh's stop rules need ~100+ outer iterations, ~15 s each
+    for the oracle at this size; the C1 golden covers the stop rules to convergence.)"""
+    from oracle import foto_oracle as O
+    Nt, Nx, Ny, r, eps, iters = 16, 584, 388, 1.0, 1e-2, 3
+    rho0, rhoT = textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+    with BBSolver(rho0, rhoT, Nt, Nx, Ny, r=r, reg_epsilon=eps) as s:
+        s.iterate(iters, 0.0, False)
+        crit, its, phi = np.array(s.crit), np.array(s.cg_its), s.phi()
+        u, v, m = s.flow()
+    st = {}
+    uo, vo, mo = O.solve(rho0, rhoT, Nt, Nx, Ny, r=r, convergence_tol=0.0, reg_epsilon=eps, max_it=iters, stats=st,
+                         log=lambda line: None, stop_rules=False)
+    print(f"C5 584x388x16: cg {its.tolist()} (oracle {st['cg_its'].tolist()}), crit rel {_rel(crit, st['crit']):.2e}, "
+          f"phi rel {_rel(phi, st['phi']):.2e}, flow {max(np.abs(a - b).max() for a, b in ((u, uo), (v, vo), (m, mo))):.2e} px")
+    assert np.max(np.abs(its - st["cg_its"])) <= 1
+    np.testing.assert_allclose(crit, st["crit"], rtol=1e-8, atol=0)
+    assert _rel(phi, st["phi"]) <= 1e-8
+    for a, b in ((u, uo), (v, vo), (m, mo)):
+        assert np.abs(a - b).max() <= 1e-7
+
+
 @pytest.mark.parametrize("mode", [3, 2, 0])
 def test_c2_shape_vs_reference(gold, mode):
     d = gold("bb_c2s.npz")
