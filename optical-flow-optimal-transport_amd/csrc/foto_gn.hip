@@ -1698,6 +1698,7 @@ struct foto_gn_plan {
     bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
     size_t pt_l0 = 0;                // first level of the persistent small-level launch (0: none; FOTO_MG_PTAIL=1: on)
     bool lt = false;                 // the last level + coarsest in one LDS-resident block (k_mg_ltail)
+    int graph_its = 4;               // PCG iterations per graph replay (FOTO_GN_GRAPH, even)
     unsigned* pt_counter = nullptr;  // its grid-barrier arrivals (zeroed per solve)
     int nb_pix = 0, nb_rz = 0;
     CGScal* dS = nullptr;
@@ -1975,10 +1976,18 @@ static int gn_plan_init(foto_gn_plan* P) {
                                                (int)bytes));
         }
     }
-    // two iterations (p0 -> p1 -> p0) captured once; the kernels read the iteration index from
-    // the device, so the graph is replayed unchanged
+    // P->graph_its iterations (p0 -> p1 -> p0 ...) captured once; the kernels read the iteration
+    // index from the device, so the graph is replayed unchanged.  Round 5: 4 instead of 2 -- a
+    // replay boundary cost ~17 us of idle GPU (profiles/r05_gn_trace.txt: 8.4 us per iteration
+    // before k_gnp_dir), and a reused plan launches its predicted count in one go either way
+    {
+        const char* e = getenv("FOTO_GN_GRAPH");
+        const int g = e ? atoi(e) : 4;
+        P->graph_its = (g >= 2 && g <= 16 && g % 2 == 0) ? g : 4;
+    }
     FOTO_HIP_CHECK(hipStreamBeginCapture(P->s, hipStreamCaptureModeThreadLocal));
-    const int c1 = gn_iteration(P, 0), c2 = c1 < 0 ? c1 : gn_iteration(P, 1);
+    int c2 = 0;
+    for (int it = 0; it < P->graph_its && c2 >= 0; ++it) c2 = gn_iteration(P, it & 1);
     const hipError_t ec = hipStreamEndCapture(P->s, &P->graph);
     FOTO_TRY(c2);
     FOTO_HIP_CHECK(ec);
@@ -2041,19 +2050,19 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     FOTO_TRY(gn_vcycle(P, P->r, P->z, P->rz_part[0]));
     FOTO_HIP_CHECK(hipEventRecord(P->ev[1], s));
     tr.mark("solve: setup enqueued");
-    // replay pairs of iterations; the first wait comes after the previous solve's count
+    // replay the graph (G = graph_its iterations); the first wait comes after the previous solve's
+    // count: the top-of-iteration test that ends a solve of `its` iterations runs in iteration
+    // its, so its + 1 iterations are launched (rounded up to whole graphs)
     int k = 0;
     bool done = false;
     const int maxiter = P->maxiter;
-    const int first = P->last_its > 0 ? P->last_its + (P->last_its & 1) : 16;
+    const int G = P->graph_its;
+    const int first = P->last_its > 0 ? ((P->last_its + 1 + G - 1) / G) * G : 16;
     while (k < maxiter) {
-        const int chunk = std::min(k == 0 ? first : 2, maxiter - k);
+        const int chunk = std::min(k == 0 ? first : G, maxiter - k);
         int j = 0;
-        for (; j + 2 <= chunk; j += 2, k += 2) FOTO_HIP_CHECK(hipGraphLaunch(P->gexec, s));
-        if (j < chunk) {   // odd maxiter: one last iteration outside the graph (k even: p0 -> p1)
-            FOTO_TRY(gn_iteration(P, 0));
-            ++k;
-        }
+        for (; j + G <= chunk; j += G, k += G) FOTO_HIP_CHECK(hipGraphLaunch(P->gexec, s));
+        for (; j < chunk; ++j, ++k) FOTO_TRY(gn_iteration(P, k & 1));   // (maxiter's remainder, outside the graph)
         FOTO_HIP_CHECK(hipMemcpyAsync(P->hS, P->dS, sizeof(CGScal), hipMemcpyDeviceToHost, s));
         if (k == chunk) FOTO_TRY(gn_staging(P));   // while the first iterations run
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
