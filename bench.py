@@ -238,7 +238,7 @@ def gn_side():
                     "us_per_pcg_it": round(1e3 * tm["ms_pcg"] / max(tm["iterations"], 1), 1),
                     "roofline": {"bound": "hbm", "alg_bytes_per_it": by, "achieved": round(ach, 1),
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                 "note": "PCG phase: 12 launches per iteration (the update folded into the level-0 down leg), small levels at the launch floor"}})
+                                 "note": "PCG phase: 10 launches per iteration (the update folded into the level-0 down leg, the last level + coarsest in one LDS-resident block), 4 iterations per graph replay, small levels at the launch floor"}})
         out[f"gpu_{w}x{h}"] = rec
     return out
 
