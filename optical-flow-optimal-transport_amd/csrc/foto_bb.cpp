@@ -165,6 +165,10 @@ struct foto_bb_ctx {
     hipEvent_t cfork = nullptr, cjoin = nullptr;
     hipEvent_t cpart[8] = {};      // the backward all-to-all's parts, landed
     bool phi_halo = false;         // phi's halo planes came with the backward all-to-all
+    // the w_t halo of the deferred slab edges, issued on sc before k_prox_rhs (wt_overlap); the
+    // next forward finishes the edge planes' F (k_rhs_edge) from it
+    bool wt_pending = false;       // issued on sc by prox_rhs, not yet consumed
+    bool wt_guarded = false;       // (the prox it belongs to was launched behind a solve's done flag)
     std::vector<std::unique_ptr<Shard>> sh;   // local shards
     CGScal* hS = nullptr;                     // pinned host mirror of shard 0's CG scalars
     int last_cg = 0;
@@ -519,6 +523,57 @@ static int a2a_halo(const foto_bb_ctx* c) {
     return (c->fuse && pe && atoi(pe) == 0) ? 0 : 1;
 }
 
+// F on the deferred edge planes of every local shard, from its w_t halo (k_rhs_edge)
+static int wt_edges(foto_bb_ctx* c, bool guarded) {
+    for (auto& sp : c->sh) {
+        Shard& s = *sp;
+        const int dlo = s.g.t0 > 0, dhi = s.g.t0 + s.g.nloc < c->Nt;
+        double* rr = c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr;
+        const int* gd = guarded ? s.spec->done_flag() : nullptr;
+        if (dlo)
+            FOTO_HIP_CHECK(launch_rhs_edge(s.g, 0, s.wt, s.edge, s.rho0, s.rhoT, c->r, s.rv, s.rb, rr, c->s, gd));
+        if (dhi && !(dlo && s.g.nloc == 1))
+            FOTO_HIP_CHECK(launch_rhs_edge(s.g, s.g.nloc - 1, s.wt, s.edge + 4 * s.g.nxy, s.rho0, s.rhoT, c->r, s.rv,
+                                           s.rb, rr, c->s, gd));
+    }
+    return 0;
+}
+
+// (round 5) the w_t exchange overlapped with k_prox_rhs: k_wt_pre computes the edge planes' w_t
+// first, the exchange travels on the communication stream while k_prox_rhs runs, and the next
+// forward finishes the edge planes' F (k_rhs_edge) before transforming them.  RCCL on its own
+// stream, a spectral CG (the stencil CG needs F.F at once), slabs of >= 3 planes;
+// FOTO_WT_OVERLAP=0: exchange and finish the edges after k_prox_rhs
+static bool slabs_of_3(const foto_bb_ctx* c) {
+    // all ranks decide alike (the call sequences stay identical whichever way, tests/test_xfer.py),
+    // so the rule rests on the smallest slab of the split
+    for (int r = 0; r < c->W; ++r) {
+        int t0 = 0, nl = 0;
+        if (split_planes(c->Nt, c->W, r, &t0, &nl) != 0 || nl < 3) return false;
+    }
+    return true;
+}
+static bool wt_overlap(const foto_bb_ctx* c) {
+    if (!c->rccl || !c->sc || c->o.cg_mode == 0 || c->sh.size() != 1 || !slabs_of_3(c)) return false;
+    const char* e = getenv("FOTO_WT_OVERLAP");
+    return !(e && atoi(e) == 0);
+}
+
+// k_wt_pre ahead of k_prox_rhs: RCCL where wt_overlap holds; virtual ranks with FOTO_WT_PRE=1
+// (the same kernel sequence, exchanged by copies on s -- tests, tools/proxy_scaling.py)
+static bool wt_pre_on(const foto_bb_ctx* c) {
+    if (c->rccl) return wt_overlap(c);
+    const char* e = getenv("FOTO_WT_PRE");
+    return c->W > 1 && c->o.cg_mode != 0 && e && atoi(e) == 1 && slabs_of_3(c);
+}
+
+// a w_t exchange that no forward will consume (a new prox supersedes it): forget or wait for it
+static int wt_drop(foto_bb_ctx* c) {
+    if (!c->wt_pending) return 0;
+    c->wt_pending = false;
+    return comm_join(c);
+}
+
 // Spectral CG over time-slab shards, in phases: x/y DCTs on the own planes, all-to-all to row
 // boxes and the t-DCT (sharded_fwd); the Gauss-compressed CG -- one all-gather of the boxes'
 // histograms, summed in rank order on every rank, and the small serial solve on every rank
@@ -531,6 +586,13 @@ static int sharded_fwd(foto_bb_ctx* c) {
     // the slab side is the shard's RHS buffer: fwd_local leaves the x / y DCTs of F there
     auto sbuf = [](Shard& s) { return s.rv; };
     auto rbuf = [](Shard& s) { return s.spec->box_in(); };
+    // w_t exchanged behind k_prox_rhs (wt_overlap; landed by now: the crit all-gather queued
+    // behind it on sc was joined): the edge planes' F before their x / y DCTs
+    if (c->wt_pending) {
+        FOTO_TRY(comm_join(c));
+        c->wt_pending = false;
+        FOTO_TRY(wt_edges(c, c->wt_guarded));
+    }
     for (int p = 0; p < parts; ++p) {
         for (auto& sp : c->sh) {
             int lo, hi;
@@ -691,6 +753,7 @@ static int outer_head(foto_bb_ctx* c) {
     // the previous iteration's k_prox_rhs wrote F (and F.F).  (Enqueuing the next solve's x-DCT
     // here, ahead of the crit wait, measured no faster: 457 vs 457 it/s same box.)
     if (c->fuse && c->f_ready) return 0;
+    FOTO_TRY(wt_drop(c));   // (F recomputed whole: no edge planes left to finish)
     FOTO_TRY(halo(c, [](Shard& s) { return s.mu[0]; }));
     FOTO_TRY(halo(c, [](Shard& s) { return s.q[0]; }));
     for (auto& sp : c->sh) {
@@ -715,6 +778,8 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
     // or recompute the neighbours' boundary stepB (FOTO_PR_EDGE=0: five planes, 2 phi + 3 mu)
     const char* pe = getenv("FOTO_PR_EDGE");
     const bool defer = W > 1 && !(pe && atoi(pe) == 0);
+    FOTO_TRY(wt_drop(c));   // (a redo's prox supersedes a pending exchange)
+    const bool pre = defer && wt_pre_on(c);
     if (W > 1) {
         if (defer) {
             if (!c->phi_halo) FOTO_TRY(halo(c, [](Shard& s) { return s.phi; }));
@@ -722,6 +787,25 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
             FOTO_TRY(exchange(c, halo_depth_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W, 2), [](Shard& s) { return s.phi; },
                               [](Shard& s) { return s.phi; }));
             for (int f = 0; f < 3; ++f) FOTO_TRY(halo(c, [f](Shard& s) { return s.fz_src[f]; }));
+        }
+    }
+    if (pre) {   // the edge planes' w_t first, then on the wire while k_prox_rhs runs
+        for (auto& sp : c->sh) {
+            Shard& s = *sp;
+            const int dlo = s.g.t0 > 0, dhi = s.g.t0 + s.g.nloc < c->Nt;
+            hipEvent_t e = c->kt.start(c->s);
+            FOTO_HIP_CHECK(launch_wt_pre(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], c->r, s.wt, dlo, dhi, c->s,
+                                         guarded ? s.spec->done_flag() : nullptr));
+            c->kt.stop(e, c->s, FOTO_K_PROX, 56.0 * (double)((dlo ? 1 : 0) + (dhi ? 1 : 0)) * (double)s.g.nxy);
+        }
+        if (c->rccl) {
+            FOTO_TRY(comm_fork(c));
+            FOTO_TRY(exchange_raw(c, halo_xfers(c->Nt, (int64_t)c->Nx * c->Ny, W), [](Shard& s) { return s.wt; },
+                                  [](Shard& s) { return s.wt; }));
+            c->wt_pending = true;
+            c->wt_guarded = guarded;
+        } else {
+            FOTO_TRY(halo(c, [](Shard& s) { return s.wt; }));
         }
     }
     for (auto& sp : c->sh) {
@@ -732,22 +816,13 @@ static int prox_rhs(foto_bb_ctx* c, bool guarded, int par) {
         FOTO_HIP_CHECK(launch_prox_rhs(s.g, s.phi, s.fz_src[0], s.fz_src[1], s.fz_src[2], s.fz_dst[0], s.fz_dst[1],
                                        s.fz_dst[2], s.rho0, s.rhoT, c->r, s.rv, s.rb, s.gath_crit(W) + 2 * s.rank,
                                        c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr, c->s,
-                                       guarded ? s.spec->done_flag() : nullptr, dlo, dhi, s.wt, s.edge, hcrit));
+                                       guarded ? s.spec->done_flag() : nullptr, dlo, dhi, s.wt, s.edge, hcrit,
+                                       pre ? 1 : 0));
         c->kt.stop(e, c->s, FOTO_K_PROX, 64.0 * nv);
     }
-    if (defer) {
-        FOTO_TRY(halo(c, [](Shard& s) { return s.wt; }));
-        for (auto& sp : c->sh) {
-            Shard& s = *sp;
-            const int dlo = s.g.t0 > 0, dhi = s.g.t0 + s.g.nloc < c->Nt;
-            double* rr = c->o.cg_mode == 0 ? s.gath_rr() + s.rank : nullptr;
-            const int* gd = guarded ? s.spec->done_flag() : nullptr;
-            if (dlo)
-                FOTO_HIP_CHECK(launch_rhs_edge(s.g, 0, s.wt, s.edge, s.rho0, s.rhoT, c->r, s.rv, s.rb, rr, c->s, gd));
-            if (dhi && !(dlo && s.g.nloc == 1))
-                FOTO_HIP_CHECK(launch_rhs_edge(s.g, s.g.nloc - 1, s.wt, s.edge + 4 * s.g.nxy, s.rho0, s.rhoT, c->r, s.rv,
-                                               s.rb, rr, c->s, gd));
-        }
+    if (defer && !c->wt_pending) {   // (RCCL with pre: the next forward finishes the edges)
+        if (!pre) FOTO_TRY(halo(c, [](Shard& s) { return s.wt; }));
+        FOTO_TRY(wt_edges(c, guarded));
     }
     c->phi_halo = false;   // (consumed: the next prox's phi comes from the next solve)
     // the stencil CG's F.F (its stopping rule) from every rank
@@ -856,6 +931,7 @@ static int rollback(foto_bb_ctx* c) {
     const foto_bb_ctx::Enq e = c->inflight.back();
     c->inflight.pop_back();
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
+    FOTO_TRY(wt_drop(c));   // (the dropped prox's w_t: the next head recomputes F whole)
     Shard& s0 = *c->sh[0];
     if (e.dsp) FOTO_TRY(e.dsp->drop_newest(c->s));
     c->kt.discard_from(e.kmark);
@@ -879,6 +955,10 @@ static int rollback(foto_bb_ctx* c) {
 // one being reported is the first), forget their deferred solves and timings, and leave no
 // record behind, so foto_bb_reset can start over.
 static void drain_inflight(foto_bb_ctx* c) {
+    if (c->sc && c->wt_pending) {   // (a pending w_t exchange: let it land, nothing consumes it)
+        (void)hipStreamSynchronize(c->sc);
+        c->wt_pending = false;
+    }
     if (c->inflight.empty()) return;
     (void)hipStreamSynchronize(c->s);
     for (auto it = c->inflight.rbegin(); it != c->inflight.rend(); ++it)

@@ -235,7 +235,12 @@ hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, c
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s,
                            const int* guard = nullptr, int defer_lo = 0, int defer_hi = 0, double* wt_out = nullptr,
-                           double* edge = nullptr, double* hcrit = nullptr);
+                           double* edge = nullptr, double* hcrit = nullptr, int wt_pre = 0);
+// w_t = mu'_t - r q_t of the deferred edge planes (0 if defer_lo, nloc - 1 if defer_hi) into
+// wt, ahead of launch_prox_rhs (which then gets wt_pre = 1 and leaves those planes alone): the
+// w_t exchange can travel while the fused kernel runs.  phi needs its halo planes.
+hipError_t launch_wt_pre(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
+                         double r, double* wt, int defer_lo, int defer_hi, hipStream_t s, const int* guard = nullptr);
 // F of a deferred edge plane n (0 or nloc - 1; edge slot 0 or 1), F.F added to gath_rr[0]
 hipError_t launch_rhs_edge(const Geo& g, int n, const double* wt, const double* edge, const double* rho0,
                            const double* rhoT, double r, double* F, RedBuf rb, double* gath_rr, hipStream_t s,

@@ -780,7 +780,8 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(PR_WPE)))
         const double* __restrict__ muy, double* __restrict__ nut, double* __restrict__ nux, double* __restrict__ nuy,
         const double* __restrict__ rho0, const double* __restrict__ rhoT, double r, double inv_r,
         double* __restrict__ F, RedBuf rb, double* gath_crit, double* gath_rr, const int* __restrict__ guard, int tch,
-        int defer_lo, int defer_hi, double* __restrict__ wt_out, double* __restrict__ edge, double* hcrit) {
+        int defer_lo, int defer_hi, double* __restrict__ wt_out, double* __restrict__ edge, double* hcrit,
+        int wt_pre) {
     if (guard && *guard == 0) return;
     __shared__ double fr[4][PR_FN];                  // phi ring (plane p in slot p & 3)
     __shared__ double wb[2][2][PR_PH * PR_PW];       // [plane & 1][x | y part] of w
@@ -978,7 +979,9 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(PR_WPE)))
             if (EDGE && own[v] && n >= l0) {
                 // what k_rhs_edge needs next to a deferred edge, from the values F(n) would use: w_t
                 // of the two outermost planes, and (w_x, w_y, mu'_t, q_t) of the edge plane itself
-                if ((defer_lo && n <= 1) || (defer_hi && n >= nl - 2)) wt_out[n * nxy + ooff[v]] = wtc[v];
+                // (wt_pre: k_wt_pre wrote the edge planes' w_t, which may be on the wire already)
+                if (((defer_lo && n <= 1) || (defer_hi && n >= nl - 2)) && !(wt_pre && deferred))
+                    wt_out[n * nxy + ooff[v]] = wtc[v];
                 if (deferred) {   // slot 0: plane 0, slot 1: plane nloc - 1 (nloc = 1: both)
                     const int ci = opy[v] * PR_PW + opx;
                     double* E = edge + ooff[v] + ((defer_lo && n == 0) ? 0 : 4 * nxy);
@@ -1050,18 +1053,56 @@ int prox_rhs_blocks(const Geo& g) {
 hipError_t launch_prox_rhs(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
                            double* nut, double* nux, double* nuy, const double* rho0, const double* rhoT, double r,
                            double* F, RedBuf rb, double* gath_crit, double* gath_rr, hipStream_t s, const int* guard,
-                           int defer_lo, int defer_hi, double* wt_out, double* edge, double* hcrit) {
+                           int defer_lo, int defer_hi, double* wt_out, double* edge, double* hcrit, int wt_pre) {
     const int nb = prox_rhs_blocks(g);
     if (rb.cap < 3 * nb) return hipErrorInvalidValue;
     if ((defer_lo || defer_hi) && (!wt_out || !edge)) return hipErrorInvalidValue;
     if (defer_lo || defer_hi)
         k_prox_rhs<true><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
                                               gath_crit, gath_rr, guard, prox_rhs_tch(g), defer_lo, defer_hi, wt_out, edge,
-                                              hcrit);
+                                              hcrit, wt_pre);
     else
         k_prox_rhs<false><<<nb, PR_NT, 0, s>>>(g, phi, mut, mux, muy, nut, nux, nuy, rho0, rhoT, r, 1.0 / r, F, rb,
                                                gath_crit, gath_rr, guard, prox_rhs_tch(g), 0, 0, nullptr, nullptr,
-                                               hcrit);
+                                               hcrit, 0);
+    return hipGetLastError();
+}
+
+// (round 5) w_t of a shard's deferred edge planes before k_prox_rhs: per voxel k_prox's stepB
+// (the fused kernel's stepb, same operations in the same order, out-of-grid neighbours 0.0 as
+// its LDS image holds them), so the w_t plane each neighbour needs can be on the wire while
+// k_prox_rhs runs (foto_bb.cpp prox_rhs / wt_overlap).  blockIdx.y: plane pa, then pb.
+__global__ __launch_bounds__(NT) void k_wt_pre(Geo g, int pa, int pb, const double* __restrict__ phi,
+                                               const double* __restrict__ mut, const double* __restrict__ mux,
+                                               const double* __restrict__ muy, double r, double inv_r,
+                                               double* __restrict__ wt, const int* __restrict__ guard) {
+    if (guard && *guard == 0) return;
+    const int64_t nxy = g.nxy;
+    const int64_t off = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (off >= nxy) return;
+    const int p = blockIdx.y == 0 ? pa : pb;
+    const int y = (int)(off / g.Nx), x = (int)(off - (int64_t)y * g.Nx), t = g.t0 + p;
+    const int64_t i = (int64_t)p * nxy + off;
+    const double c = phi[i];
+    const double tm = t > 0 ? phi[i - nxy] : 0.0, tp = t < g.Nt - 1 ? phi[i + nxy] : 0.0;
+    const double gt = d1w(t, g.Nt, tm, c, tp);
+    const double gx = d1w(x, g.Nx, x > 0 ? phi[i - 1] : 0.0, c, x < g.Nx - 1 ? phi[i + 1] : 0.0);
+    const double gy = d1w(y, g.Ny, y > 0 ? phi[i - g.Nx] : 0.0, c, y < g.Ny - 1 ? phi[i + g.Nx] : 0.0);
+    const double m0 = mut[i], m1 = mux[i], m2 = muy[i];
+    double a, b1, b2;
+    project_K(gt + inv_r * m0, gx + inv_r * m1, gy + inv_r * m2, a, b1, b2);
+    double n0 = m0 + r * (gt - a);
+    n0 = (n0 < 0.0) ? 0.0 : n0;
+    wt[i] = n0 - r * a;
+}
+
+hipError_t launch_wt_pre(const Geo& g, const double* phi, const double* mut, const double* mux, const double* muy,
+                         double r, double* wt, int defer_lo, int defer_hi, hipStream_t s, const int* guard) {
+    if (!defer_lo && !defer_hi) return hipSuccess;
+    const int pa = defer_lo ? 0 : g.nloc - 1, pb = g.nloc - 1;
+    const int np = (defer_lo && defer_hi && g.nloc > 1) ? 2 : 1;
+    k_wt_pre<<<dim3((unsigned)flat_blocks(g.nxy), np), NT, 0, s>>>(g, pa, pb, phi, mut, mux, muy, r, 1.0 / r, wt,
+                                                                  guard);
     return hipGetLastError();
 }
 

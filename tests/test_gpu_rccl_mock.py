@@ -172,14 +172,14 @@ def test_rccl_comm_stream_pipelined_alltoall_and_phi_halo(monkeypatch, W):
     Nt, Nx, Ny = 7, 48, 40
     rho0, rhoT = textured_pair(Nx, Ny, seed=5, dx=1.0, dy=0.5)
     L = _mock()
-    for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM"):
+    for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM", "FOTO_WT_OVERLAP"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("FOTO_A2A_PARTS", "1")
     monkeypatch.setenv("FOTO_A2A_HALO", "0")
     monkeypatch.setenv("FOTO_COMM_STREAM", "0")
     plain = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
     for env in ({}, {"FOTO_A2A_PARTS": "3"}, {"FOTO_A2A_HALO": "0"}, {"FOTO_COMM_STREAM": "0"}):
-        for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM"):
+        for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM", "FOTO_WT_OVERLAP"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -191,3 +191,32 @@ def test_rccl_comm_stream_pipelined_alltoall_and_phi_halo(monkeypatch, W):
             np.testing.assert_array_equal(a["phi"], b["phi"])
         for a, b in zip(ranks[0]["flow"], plain[0]["flow"]):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("W,parts", [(2, 1), (3, 2), (3, 3)])
+def test_rccl_wt_exchange_overlapped_with_interior_planes(monkeypatch, W, parts):
+    """The deferred slab edges' w_t computed first (k_wt_pre) and exchanged on the communication
+    stream while k_prox_rhs runs, the edges' F finished by the next forward (foto_bb.cpp
+    wt_overlap / prox_rhs / sharded_fwd), equals the prox-then-exchange order (FOTO_WT_OVERLAP=0)
+    bit for bit, and the virtual ranks with and without k_wt_pre.  Nt = 10: slabs of three and
+    four planes (the overlap needs >= 3 on every rank)."""
+    from foto.synthetic import textured_pair
+    Nt, Nx, Ny = 10, 48, 40
+    rho0, rhoT = textured_pair(Nx, Ny, seed=7, dx=0.5, dy=1.0)
+    L = _mock()
+    for k in ("FOTO_A2A_HALO", "FOTO_COMM_STREAM"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("FOTO_A2A_PARTS", str(parts))
+    monkeypatch.setenv("FOTO_WT_OVERLAP", "0")
+    seq = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    monkeypatch.setenv("FOTO_WT_OVERLAP", "1")
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    compare(ranks, virt, Nt, Nx, Ny, W)
+    monkeypatch.setenv("FOTO_WT_PRE", "1")   # virtual ranks with k_wt_pre (tools/proxy_scaling.py)
+    compare(ranks, run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3), Nt, Nx, Ny, W)
+    for a, b in zip(ranks, seq):
+        assert a["crit"] == b["crit"] and a["cg"] == b["cg"]
+        np.testing.assert_array_equal(a["phi"], b["phi"])
+    for a, b in zip(ranks[0]["flow"], seq[0]["flow"]):
+        np.testing.assert_array_equal(a, b)

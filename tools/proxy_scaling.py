@@ -19,7 +19,9 @@ foto_bb.cpp sharded_fwd / sharded_inv / prox_rhs):
     of PARTS equal parts takes C/P + (P-1) max(C, M)/P + M/P for compute C and transfer M;
   * the box -> slab all-to-all likewise, carrying phi's halo planes (one per side) as well, so
     the inverse x / y DCTs run on nloc + 2 planes (their extra compute is added);
-  * the w_t halo of the deferred slab edges: one plane with each neighbour (both at once);
+  * the w_t halo of the deferred slab edges: one plane with each neighbour (both at once),
+    issued before k_prox_rhs (k_wt_pre) so that only what outlasts the measured prox time is
+    exposed (FOTO_WT_OVERLAP=0: all of it; the virtual shards run k_wt_pre, FOTO_WT_PRE=1);
   * the 32-KB histogram all-gather and the crit all-gather;
 at LINK_GBS per direction per link and LAT_US per RCCL call.  --no-overlap prints round 4's
 model (phi halo a separate plane per neighbour, nothing overlapped) for comparison.
@@ -53,6 +55,11 @@ def a2a_setup():
     return max(1, min(8, parts)), halo
 
 
+def wt_overlap_on(W):
+    """foto_bb.cpp wt_overlap: every slab of >= 3 planes, FOTO_WT_OVERLAP not 0."""
+    return NT // W >= 3 and os.environ.get("FOTO_WT_OVERLAP", "1") != "0"
+
+
 def pipe_us(c_us, m_us, parts):
     """A two-stage pipeline (compute then transfer, or transfer then compute) of `parts` equal
     parts: the time beyond the compute alone."""
@@ -60,9 +67,10 @@ def pipe_us(c_us, m_us, parts):
     return c_us / p + (p - 1) * max(c_us, m_us) / p + m_us / p - c_us
 
 
-def comm_model_us(W, slab_ms=0.0, overlap=True):
+def comm_model_us(W, slab_ms=0.0, overlap=True, prox_ms=0.0):
     """Modelled communication time per rank per outer iteration that the compute does not hide
-    (see the docstring).  slab_ms: the rank's measured slab-side x / y DCT time (both directions)."""
+    (see the docstring).  slab_ms: the rank's measured slab-side x / y DCT time (both directions);
+    prox_ms: its measured k_wt_pre + k_prox_rhs time (the w_t exchange travels behind it)."""
     if W == 1:
         return 0.0, {}
     nl = -(-NT // W)                          # the largest slab
@@ -77,10 +85,15 @@ def comm_model_us(W, slab_ms=0.0, overlap=True):
     c = 1e3 * slab_ms / 2                     # x / y DCTs of one direction (measured: incl. the halo
     #                                           planes' inverse DCTs when they are delivered)
     a2a_i = (nl + 2 * halo) * plane * (W - 1) / W / links / bw   # + phi's two halo planes
+    # w_t (foto_bb.cpp wt_overlap, slabs of >= 3 planes, FOTO_WT_OVERLAP=0: off) travels while
+    # k_prox_rhs runs (the crit all-gather behind it on the communication stream is joined next)
+    wt = plane / bw + LAT_US
+    if wt_overlap_on(W):
+        wt = max(0.0, wt - 1e3 * prox_ms)
     parts = {"alltoall_fwd": pipe_us(c, a2a, P) + P * LAT_US,
              "alltoall_inv": pipe_us(c, a2a_i, P) + P * LAT_US,
              "halo_phi": 0.0 if halo else plane / bw + LAT_US,
-             "halo_wt": plane / bw + LAT_US,
+             "halo_wt": wt,
              "allgathers": 2 * LAT_US}
     return sum(parts.values()), parts
 
@@ -120,6 +133,8 @@ def main():
     args = ap.parse_args()
     global NX, NY, NT
     NX, NY, NT = (1024, 1024, 64) if args.grid == "c4" else (int(v) for v in args.grid.split(","))
+    if not args.no_overlap and os.environ.get("FOTO_WT_OVERLAP", "1") != "0":
+        os.environ["FOTO_WT_PRE"] = "1"   # the virtual shards run k_wt_pre as the RCCL ranks would
     rows = [measure(int(w), args.steps, args.warmup) for w in args.worlds.split(",")]
     base = rows[0]["rank_ms"] * rows[0]["W"]
     lines = [f"# compute-only proxy, {NX}x{NY}x{NT}, r={R}, eps={EPS}: per-rank kernel time of W virtual shards on one",
@@ -131,7 +146,8 @@ def main():
     for r in rows:
         k = r["kernels_ms"]
         eff = base / (r["W"] * r["rank_ms"])
-        cm, parts = comm_model_us(r["W"], k.get("dct_slab", 0.0), overlap=not args.no_overlap)
+        cm, parts = comm_model_us(r["W"], k.get("dct_slab", 0.0), overlap=not args.no_overlap,
+                                  prox_ms=k.get("prox", 0.0))
         r["comm_model_us"] = {"total": cm, **parts}
         model_ms = r["rank_ms"] + cm / 1e3
         lines.append(f"  {r['W']:>2} {r['rank_ms']:10.3f} {1e3 / r['rank_ms']:10.1f} {eff:5.2f} {r['cg_its']:6.1f} "
@@ -147,7 +163,7 @@ def main():
         lines.append(f"# comm model (round 5): the all-to-alls in {P} part(s) on the communication stream, pipelined "
                      f"against the slab-side x / y DCTs (dct_slab, measured), phi's halo planes "
                      f"{'inside the backward all-to-all (their inverse DCT is in the measured compute)' if halo else 'as one plane per neighbour'}, "
-                     f"w_t one plane per neighbour, {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
+                     f"w_t one plane per neighbour{' behind k_prox_rhs (k_wt_pre in the measured prox)' if wt_overlap_on(2) else ''}, {LINK_GBS:.0f} GB/s per link direction, {LAT_US:.0f} us per RCCL call "
                      f"(a model, not a measurement).")
     lines.append("# cg: the CG kernels as timed by the library (mode 3: the Gauss-compressed CG's histogram and "
                  "node solve groups; mode 2: the s-step passes, incl. a deferred solve's no-op margin passes).")
