@@ -85,7 +85,8 @@ __device__ bool gn_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
 // PCG kernels run a grid-stride loop over pixels on at most two blocks per CU: each block
 // adds one agent-scope ticket per launch, and 1200 tickets on one address (one block per
 // 256 pixels at 640x480) serialised at the memory side (~28 us per kernel, rocprofv3); with
-// 512 blocks and a 512-entry gather the kernels are bandwidth-bound.
+// 512 blocks and a 512-entry gather the kernels are bandwidth-bound.  (Round 5: 3, 4 or 5
+// blocks per CU measured the same, 113.4-114.2 us per PCG iteration, profiles/r05_gn_trace.txt.)
 static int gn_grid(int64_t n) {
     static int cap = 0;
     if (cap == 0) {
@@ -774,6 +775,12 @@ struct MGUpd {
 //   r = f - A x over the tile + 1 halo cell                                   -> LDS; x -> xg
 //   fc = R r = P^T r / 4 for the tile's GT_Y/2 x GT_X/2 coarse cells (4 x 4 taps) -> fc
 // UPD (level 0 of a PCG iteration): f is r' = r - alpha q, formed here (MGUpd above)
+#ifndef FOTO_MG_B2LATE
+#define FOTO_MG_B2LATE 1
+#endif
+#ifndef FOTO_MG_RSALIAS
+#define FOTO_MG_RSALIAS 1
+#endif
 template <bool UPD>
 __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const CGScal* S,
                                                  const double* __restrict__ f, double* __restrict__ xg,
@@ -785,21 +792,33 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
     constexpr int C1 = (XH * XW + NT - 1) / NT, C2 = (RH * RW + NT - 1) / NT;
     __shared__ double xs[3][XH][XW];
     __shared__ double fs[3][XH][XW];
+#if FOTO_MG_RSALIAS
+    // r lives in fs's space (fs is dead once stage 2 has read it; one barrier more): 49 -> 35 KB
+    // of LDS per block, four blocks per CU instead of three
+    static_assert(3 * RH * RW <= 3 * XH * XW, "r fits f's space");
+    double (*rs)[RH][RW] = reinterpret_cast<double (*)[RH][RW]>(&fs[0][0][0]);
+#else
     __shared__ double rs[3][RH][RW];
+#endif
     const int done = S->done;
     const int w = L.w, h = L.h;
     const int64_t n = (int64_t)w * h;
     const int tiles_x = (w + GT_X - 1) / GT_X;
     const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
-    // stage-2 cells' B (tile + 1 halo)
+    // stage-2 cells' B (tile + 1 halo); level 0 of a PCG iteration (UPD, FOTO_MG_B2LATE=1): after
+    // stage 1 -- held from the start beside the stage-1 loads it took 150 VGPRs (3 waves per SIMD)
     double b2[C2][6];
+    auto load_b2 = [&]() {
 #pragma unroll
-    for (int k = 0; k < C2; ++k) {
-        const int c = threadIdx.x + k * NT;
-        const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
-        if (c < RH * RW && gx >= 0 && gx < w && gy >= 0 && gy < h) mg_load6(L.B, n, (int64_t)gy * w + gx, b2[k]);
-        else { for (int q = 0; q < 6; ++q) b2[k][q] = 0.0; }
-    }
+        for (int k = 0; k < C2; ++k) {
+            const int c = threadIdx.x + k * NT;
+            const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+            if (c < RH * RW && gx >= 0 && gx < w && gy >= 0 && gy < h) mg_load6(L.B, n, (int64_t)gy * w + gx, b2[k]);
+            else { for (int q = 0; q < 6; ++q) b2[k][q] = 0.0; }
+        }
+    };
+    constexpr bool B2LATE = UPD && FOTO_MG_B2LATE;
+    if constexpr (!B2LATE) load_b2();
     // stage-1 cells' f (UPD: r and q) and D^-1 (tile + 2 halo)
     double f1[C1][3], d1[C1][6];
 #pragma unroll
@@ -858,11 +877,14 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
         xs[0][ly][lx] = z0; xs[1][ly][lx] = z1; xs[2][ly][lx] = z2;
         fs[0][ly][lx] = f1[k][0]; fs[1][ly][lx] = f1[k][1]; fs[2][ly][lx] = f1[k][2];
     }
+    if constexpr (B2LATE) load_b2();
     __syncthreads();
     double rr = 0.0;
+    double rv[C2][3];
 #pragma unroll
     for (int k = 0; k < C2; ++k) {
         const int c = threadIdx.x + k * NT;
+        rv[k][0] = rv[k][1] = rv[k][2] = 0.0;
         if (c >= RH * RW) continue;
         const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
         double r0 = 0.0, r1 = 0.0, r2 = 0.0;
@@ -887,7 +909,17 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
                 }
             }
         }
-        rs[0][ly][lx] = r0; rs[1][ly][lx] = r1; rs[2][ly][lx] = r2;
+        rv[k][0] = r0; rv[k][1] = r1; rv[k][2] = r2;
+    }
+#if FOTO_MG_RSALIAS
+    __syncthreads();   // (every read of fs done)
+#endif
+#pragma unroll
+    for (int k = 0; k < C2; ++k) {
+        const int c = threadIdx.x + k * NT;
+        if (c >= RH * RW) continue;
+        const int ly = c / RW, lx = c - ly * RW;
+        rs[0][ly][lx] = rv[k][0]; rs[1][ly][lx] = rv[k][1]; rs[2][ly][lx] = rv[k][2];
     }
     __syncthreads();
     const int64_t nc = (int64_t)wc * hc;
