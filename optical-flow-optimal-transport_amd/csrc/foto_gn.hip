@@ -85,8 +85,7 @@ __device__ bool gn_reduce_last(double (&v)[K], RedBuf rb, double (&tot)[K]) {
 // PCG kernels run a grid-stride loop over pixels on at most two blocks per CU: each block
 // adds one agent-scope ticket per launch, and 1200 tickets on one address (one block per
 // 256 pixels at 640x480) serialised at the memory side (~28 us per kernel, rocprofv3); with
-// 512 blocks and a 512-entry gather the kernels are bandwidth-bound.  (Round 5: 3, 4 or 5
-// blocks per CU measured the same, 113.4-114.2 us per PCG iteration, profiles/r05_gn_trace.txt.)
+// 512 blocks and a 512-entry gather the kernels are bandwidth-bound.
 static int gn_grid(int64_t n) {
     static int cap = 0;
     if (cap == 0) {
