@@ -1,6 +1,6 @@
 """Drop-in for the reference's batch pipeline ``run.sh`` (run.sh:1-167), sharded over GPUs.
 
-    python run.py [download | install | prepare | restart | run] [--gpus N] [--data data] [--results results]
+    python run.py [download | install | prepare | restart | run] [--gpus N] [--per-gpu K] [--data data] [--results results]
 
 Same data layout, same per-sequence outputs, same ``.out.gn.sucess`` / ``.out.foto.sucess``
 skip markers (run.sh:98-117, 135-154), same hyper-parameters (run.sh:103, 114):
@@ -14,7 +14,8 @@ Differences from run.sh, all deliberate:
     (HIP_VISIBLE_DEVICES=i).  Worker i takes the sequences at positions i, i+N, ... of
     the sorted (dataset, sequence) list.  ``--devices LIST`` (or FOTO_RUN_DEVICES=LIST, e.g.
     ``0,0,1,1``) maps worker i to device LIST[i mod len]: several workers can share a GPU, so
-    one solve's latency-bound serial kernels overlap another's bandwidth-bound ones.  Under torch.distributed.run the RANK /
+    one solve's latency-bound serial kernels overlap another's bandwidth-bound ones
+    (``--per-gpu K``: K workers on each of the N GPUs).  Under torch.distributed.run the RANK /
     WORLD_SIZE / LOCAL_RANK environment picks the shard instead.  No collective is
     involved: the workers share nothing but the file system.
   * Each worker runs main.py in-process (main.main(argv)), one HIP context per worker,
@@ -382,15 +383,16 @@ def run(args):
         return rc
     if args.worker_rank is not None:
         return worker(args, args.worker_rank, args.gpus, -1)
-    if args.gpus <= 1:
+    nw = args.gpus * max(1, args.per_gpu)
+    if nw <= 1:
         rc = worker(args, 0, 1, -1)
     else:
         # one child per worker; this process never touches the device
         devs = worker_devices(args)
         procs = []
-        for i in range(args.gpus):
+        for i in range(nw):
             env = dict(os.environ, HIP_VISIBLE_DEVICES=str(devs[i % len(devs)]))
-            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "run", f"--gpus={args.gpus}",
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "run", f"--gpus={nw}",
                                            f"--worker-rank={i}", *forward_args(args)], env=env))
         rc = max(p.wait() for p in procs)
     summarize(args)
@@ -424,6 +426,9 @@ def build_parser():
     p = argparse.ArgumentParser(description="batch pipeline (run.sh)")
     p.add_argument("command", nargs="?", default="run", choices=["download", "install", "prepare", "restart", "run"])
     p.add_argument("--gpus", type=int, default=1, help="worker processes, one per GPU (see --devices)")
+    p.add_argument("--per-gpu", type=int, default=1,
+                   help="workers per GPU: --gpus N --per-gpu K starts N*K workers, worker i on device i mod N "
+                        "(two per MI355X: 10.5-10.8 vs 7.4-7.6 sequences/s, profiles/r05_c5_workers_32seq.txt)")
     p.add_argument("--devices", default=None,
                    help="comma list of device ordinals, worker i on entry i mod len (default: worker i on "
                         "device i; env FOTO_RUN_DEVICES); e.g. --gpus 2 --devices 0,0: two workers share GPU 0")

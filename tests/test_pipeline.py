@@ -280,6 +280,11 @@ def test_worker_device_map(tmp_path, monkeypatch):
     assert pipeline.main(["run", "--gpus=4", "--devices=0,0,1", *common]) == 0
     assert [d for _, d in started] == ["0", "0", "1", "0"]
     started.clear()
+    started.clear()
+    assert pipeline.main(["run", "--gpus=2", "--per-gpu=2", *common]) == 0   # 4 workers, 2 per GPU
+    assert [d for _, d in started] == ["0", "1", "0", "1"]
+    assert all("--gpus=4" in c for c, _ in started)
+    started.clear()
     monkeypatch.setenv("FOTO_RUN_DEVICES", "5,5")
     assert pipeline.main(["run", "--gpus=2", *common]) == 0
     assert [d for _, d in started] == ["5", "5"]
