@@ -993,14 +993,14 @@ __device__ __forceinline__ FftLines fft_lines(int outer, int inner) {
 // Phase loops run a compile-time number of rounds over idx = tid + 256 j (predicated), so a
 // thread's global loads are all issued before the first is consumed: a tid-strided runtime
 // loop compiled to load -> wait -> LDS store per element, one load in flight per thread.
-template <int COUNT>
+template <int COUNT, int NTH = 256>
 struct FftRounds {
-    static constexpr int R = (COUNT + 255) / 256;
-    static __device__ __forceinline__ bool ok(int idx) { return COUNT % 256 == 0 || idx < COUNT; }
+    static constexpr int R = (COUNT + NTH - 1) / NTH;
+    static __device__ __forceinline__ bool ok(int idx) { return COUNT % NTH == 0 || idx < COUNT; }
 };
 
-template <int M1, int M2, bool CONTIG>
-__global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
+template <int M1, int M2, bool CONTIG, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_dct_fft_fwd(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2, CONTIG>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
@@ -1014,20 +1014,20 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     if constexpr (LdsPrime<M2>::value)
-        for (int p = tid; p < 2 * M2; p += 256) CS[p] = tab[6 * M + 6 + p];
+        for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
     };
 #if FOTO_FFT_TW_LDS
-    for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
+    for (int p = tid; p < 2 * M; p += NTH) TW[p] = tab[p];
 #endif
     {   // load (all rounds' loads in flight), then store in Makhoul order
-        using RD = FftRounds<LPB * N>;
+        using RD = FftRounds<LPB * N, NTH>;
         double xv[RD::R];
 #pragma unroll
         for (int j0 = 0; j0 < RD::R; ++j0) {
-            const int idx = tid + 256 * j0;
+            const int idx = tid + NTH * j0;
             int l, j;
             if (CONTIG) { l = idx / N; j = idx - l * N; }
             else { j = idx / LPB; l = idx - j * LPB; }
@@ -1035,7 +1035,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
         }
 #pragma unroll
         for (int j0 = 0; j0 < RD::R; ++j0) {
-            const int idx = tid + 256 * j0;
+            const int idx = tid + NTH * j0;
             if (!RD::ok(idx)) continue;
             int l, j;
             if (CONTIG) { l = idx / N; j = idx - l * N; }
@@ -1045,17 +1045,17 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
         }
     }
     __syncthreads();
-    fft_stage1<M1, M2, false, LPB>(L, TW);
+    fft_stage1<M1, M2, false, LPB, NTH>(L, TW);
     __syncthreads();
-    fft_stage2_any<M1, M2, false, LPB>(L, CS);
+    fft_stage2_any<M1, M2, false, LPB, NTH>(L, CS);
     __syncthreads();
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double s0 = PB[2 * (M + 1)], s = PB[2 * (M + 1) + 1];
-    using RO = FftRounds<LPB * (M + 1)>;
+    using RO = FftRounds<LPB * (M + 1), NTH>;
 #pragma unroll
     for (int j0 = 0; j0 < RO::R; ++j0) {
-        const int idx = tid + 256 * j0;
+        const int idx = tid + NTH * j0;
         if (!RO::ok(idx)) continue;
         int l, k;
         if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
@@ -1076,8 +1076,8 @@ __global__ __launch_bounds__(256) void k_dct_fft_fwd(int outer, int inner, const
     }
 }
 
-template <int M1, int M2, bool CONTIG>
-__global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const double* __restrict__ tab,
+template <int M1, int M2, bool CONTIG, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const double* __restrict__ tab,
                                                      const double* __restrict__ in, double* __restrict__ out) {
     using G = FftGeom<M1, M2, CONTIG>;
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
@@ -1091,13 +1091,13 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     const int tid = threadIdx.x;
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     if constexpr (LdsPrime<M2>::value)
-        for (int p = tid; p < 2 * M2; p += 256) CS[p] = tab[6 * M + 6 + p];
+        for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
     };
 #if FOTO_FFT_TW_LDS
-    for (int p = tid; p < 2 * M; p += 256) TW[p] = tab[p];
+    for (int p = tid; p < 2 * M; p += NTH) TW[p] = tab[p];
 #endif
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
@@ -1107,11 +1107,11 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     // global reads of one Z per thread (L2-resident lines, read straight from global; no LDS
     // image of X, so Z is written once and nothing is held in registers across a barrier)
     constexpr int MH = M / 2 + 1;
-    using RP = FftRounds<LPB * MH>;
+    using RP = FftRounds<LPB * MH, NTH>;
     double xk[RP::R], xnk[RP::R], xmk[RP::R], xpk[RP::R];   // X_k, X_{N-k}, X_{M-k}, X_{N-M+k}
 #pragma unroll
     for (int j0 = 0; j0 < RP::R; ++j0) {   // all rounds' loads first
-        const int idx = tid + 256 * j0;
+        const int idx = tid + NTH * j0;
         int l, k;
         if (CONTIG) { l = idx / MH; k = idx - l * MH; }
         else { k = idx / LPB; l = idx - k * LPB; }
@@ -1126,7 +1126,7 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
     }
 #pragma unroll
     for (int j0 = 0; j0 < RP::R; ++j0) {
-        const int idx = tid + 256 * j0;
+        const int idx = tid + NTH * j0;
         if (!RP::ok(idx)) continue;
         int l, k;
         if (CONTIG) { l = idx / MH; k = idx - l * MH; }
@@ -1164,15 +1164,15 @@ __global__ __launch_bounds__(256) void k_dct_fft_inv(int outer, int inner, const
         }
     }
     __syncthreads();
-    fft_stage1<M1, M2, true, LPB>(L, TW);
+    fft_stage1<M1, M2, true, LPB, NTH>(L, TW);
     __syncthreads();
-    fft_stage2_any<M1, M2, true, LPB>(L, CS);
+    fft_stage2_any<M1, M2, true, LPB, NTH>(L, CS);
     __syncthreads();
     constexpr double iM = 1.0 / M;
-    using RS = FftRounds<LPB * N>;
+    using RS = FftRounds<LPB * N, NTH>;
 #pragma unroll
     for (int j0 = 0; j0 < RS::R; ++j0) {   // x_i = v_p, p = Makhoul position of i
-        const int idx = tid + 256 * j0;
+        const int idx = tid + NTH * j0;
         if (!RS::ok(idx)) continue;
         int l, i;
         if (CONTIG) { l = idx / N; i = idx - l * N; }
@@ -1224,6 +1224,14 @@ static std::vector<double> fft_table(int n) {
 }
 
 static int g_dct_fft = -1;   // FOTO_DCT_FFT=0 selects the GEMM kernels (A/B runs)
+// threads per block of the contiguous (x) and strided (y, t) axis passes (A/B builds)
+#ifndef FOTO_FFT_NTH_C
+#define FOTO_FFT_NTH_C 256
+#endif
+#ifndef FOTO_FFT_NTH_S
+#define FOTO_FFT_NTH_S 256
+#endif
+constexpr int FFT_NTH_C = FOTO_FFT_NTH_C, FFT_NTH_S = FOTO_FFT_NTH_S;
 
 // FFT path along one axis of [outer][n][inner]; hipErrorNotSupported if n has no instantiation
 static hipError_t dct_fft_axis(int outer, int n, int inner, bool inv, const double* tab, const double* in,
@@ -1241,11 +1249,11 @@ static hipError_t dct_fft_axis(int outer, int n, int inner, bool inv, const doub
         const int LPB = contig ? FftGeom<A, B, true>::LPB : FftGeom<A, B, false>::LPB;             \
         const int nb = contig ? (outer + LPB - 1) / LPB : outer * ((inner + LPB - 1) / LPB);       \
         if (contig) {                                                                              \
-            if (inv) k_dct_fft_inv<A, B, true><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);     \
-            else k_dct_fft_fwd<A, B, true><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);         \
+            if (inv) k_dct_fft_inv<A, B, true, FFT_NTH_C><<<nb, FFT_NTH_C, 0, s>>>(outer, inner, tab, in, out); \
+            else k_dct_fft_fwd<A, B, true, FFT_NTH_C><<<nb, FFT_NTH_C, 0, s>>>(outer, inner, tab, in, out);     \
         } else {                                                                                   \
-            if (inv) k_dct_fft_inv<A, B, false><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);    \
-            else k_dct_fft_fwd<A, B, false><<<nb, 256, 0, s>>>(outer, inner, tab, in, out);        \
+            if (inv) k_dct_fft_inv<A, B, false, FFT_NTH_S><<<nb, FFT_NTH_S, 0, s>>>(outer, inner, tab, in, out); \
+            else k_dct_fft_fwd<A, B, false, FFT_NTH_S><<<nb, FFT_NTH_S, 0, s>>>(outer, inner, tab, in, out);     \
         }                                                                                          \
         return hipGetLastError();                                                                  \
     }
