@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the FOTO_GQ_XLAB lab switch was removed from foto_gauss.inc after this measurement; results in profiles/r05_xhat_mono_ab.txt)
 # (lab) k_gq_xhat without its Clenshaw (1) or without bins and Clenshaw (2): what the kernel's loads
 # and stores cost alone -- kernel trace of the default bench with each lab build (results wrong)
 set -o pipefail
