@@ -1,32 +1,37 @@
 #!/usr/bin/env python3
 """FOTO hot-path benchmark: Benamou-Brenier outer iterations/s on the 640x480x32 grid.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1|2|3] [--mode batch|sharded]
-                    [--no-cpu-baseline] [--no-gn] [--no-strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cg-mode 0|1|2|3]
+                    [--no-cpu-baseline] [--no-gn] [--no-stencil] [--no-batch] [--no-c4]
 
 A "step" is one outer iteration of benamou_brenier.solve (benamou_brenier.py:204-258:
 RHS + CG Poisson solve + stepB/stepC + criterion) over the synthetic 640x480x32
 translating-Gaussian pair (SURVEY.md §8(d) S-metric; r = 1, eps = 1e-2, run.sh:114
 parameters), with every input and all solver state resident in HBM.  The stop rules are
-disabled so exactly K steps run.  With N > 1 (torch.distributed.run, one process per GPU):
-  * --mode batch (default; "scaling": "weak"): every GPU solves its own 640x480x32 pair, as
-    run.py streams independent sequences over GPUs (config 5, run.sh:81-157); value = the outer
-    iterations of all N solves per second (whole job), the slowest rank's clock.  The same run
-    then also measures the "strong" object: ONE problem time-sharded over the N GPUs (config 4's
-    decomposition: N time slabs, the slab <-> row-box all-to-alls and halos over RCCL), its
-    outer iterations per second -- guarded by a watchdog (FOTO_BENCH_STRONG_TIMEOUT, 180 s) so
-    a stuck collective cannot cost the headline line;
-  * --mode sharded: that time-sharded strong-scaling run as the headline ("scaling": "strong").
-At N = 1 both are the single-GPU solve.
+disabled so exactly K steps run.
 
-At N = 1 the line also carries a "gn" object: the GN baseline (classical.py)
-solved on the GPU at 640x480 (and 320x240), and the oracle's SuperLU solve of the 640x480 pair
-on one host core beside it (~75 s, run next to the BB CPU baseline on another core).
+N = 1: the single-GPU solve; the line also carries a "gn" object (the GN baseline, classical.py,
+SURVEY.md config 3, at 640x480 and 320x240 with the oracle's SuperLU solve beside it), the
+literal stencil-CG rate and the CPU baseline (the oracle on one host core).
+
+N > 1 (torch.distributed.run, one process per GPU): the headline is north_star's decomposition --
+ONE 640x480x32 solve time-sharded over the N GPUs (N time slabs; the slab <-> row-box all-to-alls,
+the phi / w_t halos and the histogram all-gather over RCCL), "scaling": "strong",
+value = its outer iterations per second on the slowest rank's clock.  It runs in a child process
+per rank under a watchdog (FOTO_BENCH_SHARD_TIMEOUT, 180 s): if RCCL fails or hangs on any rank,
+value is null and the line says why -- it is never replaced by another number.  Side objects:
+  * "c4": BASELINE config 4, the 1024x1024x64 pair time-sharded over the same N GPUs (its own
+    child per rank, its own communicator);
+  * "batch": N independent 640x480x32 solves, one per GPU (config 5's shape: run.py streams
+    independent sequences), value = all N solves' outer iterations per second -- weak scaling,
+    no collective in its data path.
+"rccl_ranks" is ncclCommCount of every rank's communicator (the line checks they agree).
 
 Multi-GPU runs need no PyTorch: the ranks (launched by torch.distributed.run, which only sets
 RANK / WORLD_SIZE / LOCAL_RANK) meet through files in a directory keyed by the launcher's
-MASTER_PORT and process id (FileRendezvous): rank 0's RCCL unique id, the barriers and the
-max-over-ranks timing.
+MASTER_PORT and process id (FileRendezvous): the RCCL unique id, the barriers and the
+max-over-ranks timing.  FOTO_BENCH_MOCK_RCCL=1 (tests only): rank 0's child runs all N ranks as
+threads over libfoto_mockrccl.so on one device (tests/test_gpu_bench.py).
 
 Prints ONE JSON line on rank 0.
 """
@@ -62,11 +67,12 @@ def parse():
     ap.add_argument("--gn-cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch HIP-event pass (roofline fields become null)")
-    ap.add_argument("--mode", choices=["batch", "sharded"], default="batch",
-                    help="N > 1: batch = one solve per GPU (weak scaling, default); sharded = one solve time-sharded "
-                         "over the N GPUs (strong scaling)")
-    ap.add_argument("--no-strong", action="store_true", help="N > 1, batch mode: skip the time-sharded side run")
-    ap.add_argument("--strong-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-batch", action="store_true", help="N > 1: skip the data-parallel side object")
+    ap.add_argument("--no-c4", action="store_true", help="N > 1: skip the config-4 (1024x1024x64) sharded side run")
+    ap.add_argument("--c4-steps", type=int, default=20)
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--shard-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--grid", type=int, nargs=3, default=[NX, NY, NT], help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -119,7 +125,10 @@ class FileRendezvous:
     def _wait(self, paths):
         t0 = time.perf_counter()
         spin = 0
+        ab = os.path.join(self.dir, "abort")
         while not all(os.path.exists(p) for p in paths):
+            if os.path.exists(ab):   # a peer failed (abort): no point waiting for it
+                raise RuntimeError(f"rendezvous {self.dir}: a peer aborted: {open(ab).read()[:300]}")
             spin += 1
             if spin > 2000:
                 time.sleep(0.0002)
@@ -152,6 +161,21 @@ class FileRendezvous:
         names = [os.path.join(self.dir, f"max{self.n}_{g}") for g in range(self.world)]
         self._wait(names)
         return max(float(open(p).read()) for p in names)
+
+    def abort(self, msg):
+        """Tell every rank still waiting in this rendezvous that this one failed."""
+        try:
+            self._put("abort", f"rank {self.rank}: {msg}".encode())
+        except OSError:
+            pass
+
+    def gather(self, value):
+        """Every rank's JSON-able value, in rank order, on every rank."""
+        self.n += 1
+        self._put(f"gat{self.n}_{self.rank}", json.dumps(value).encode())
+        names = [os.path.join(self.dir, f"gat{self.n}_{g}") for g in range(self.world)]
+        self._wait(names)
+        return [json.loads(open(p).read()) for p in names]
 
     def close(self):
         """Every rank but 0 leaves its final file and returns at once; rank 0 waits for all of
@@ -374,125 +398,250 @@ def survey_bytes(k):
     return (21 + 10 * k) * NX * NY * NT * 8
 
 
-def strong_side(args, rdv, rank, world, local_rank):
-    """Batch mode, N > 1: ONE solve time-sharded over the N GPUs (config 4's decomposition over
-    RCCL) on the same workload, run by a child process per rank (`--strong-child`): warmup,
-    barrier, K timed outer iterations, the slowest rank's clock.  Each rank waits for its child
-    at most FOTO_BENCH_STRONG_TIMEOUT s (default 180) and kills it after that -- a collective that
-    never completes, or a crash inside RCCL, cannot cost the data-parallel headline, which this
-    process prints either way (the RCCL calls have run only through the in-process transport
-    before, never across GPUs)."""
-    import subprocess
-    limit = float(os.environ.get("FOTO_BENCH_STRONG_TIMEOUT", "180"))
-    env = dict(os.environ, FOTO_BENCH_RDV_DIR=os.path.join(rdv.dir, "strong"), FOTO_BENCH_PARENT_RDV=rdv.dir,
-               FOTO_BENCH_LOCAL_DEVICE=str(local_rank))
-    cmd = [sys.executable, os.path.abspath(__file__), "--strong-child", "--gpus", str(world), "--steps",
-           str(args.steps), "--warmup", str(args.warmup), "--cg-mode", str(args.cg_mode)]
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    try:
-        out, err = proc.communicate(timeout=limit)
-    except subprocess.TimeoutExpired:
-        proc.kill()   # (this rank's own child, by its handle)
-        proc.communicate()
-        return {"error": f"timeout after {limit:.0f} s"}
-    if proc.returncode != 0:
-        tail = (err or "").strip().splitlines()[-3:]
-        return {"error": f"strong side run exited {proc.returncode}: {' | '.join(tail)}"[:300]}
-    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
-    if rank != 0:
-        return None
-    return json.loads(lines[-1]) if lines else {"error": "no result line"}
+# ------------------------------------------------------------------- N > 1: the time-sharded solve
+
+# DESIGN.md §5's model of the time-sharded solve (each rank's compute measured as virtual shards on
+# one MI355X, plus the two all-to-alls, the halos and the all-gathers at 64 GB/s per xGMI link
+# direction and 10 us per RCCL call; profiles/r05_proxy_scaling_wt.txt, r05_proxy_scaling_c4_wt.txt):
+# the curve a measured N-GPU line is read against.  The metric grid's transposition moves more
+# bytes per link than the single GPU needs for a whole outer iteration at W = 2, so the model puts
+# W = 2 below one GPU there.
+MODEL_IT_S = {(640, 480, 32): {1: 1721, 2: 886, 4: 1729, 8: 2317},
+              (1024, 1024, 64): {1: 304, 2: 170, 4: 487, 8: 1067}}
+C4_GRID = (1024, 1024, 64)   # BASELINE config 4: the 1024x1024 pair, 64 time steps, time-sharded
 
 
-def strong_child(args):
-    """The strong side run's worker (one per rank, started by strong_side): its own rendezvous
-    directory inside the parent's, the RCCL id rank 0's parent broadcast, the same workload."""
-    world = int(os.environ["WORLD_SIZE"])
-    rank = int(os.environ["RANK"])
-    device = int(os.environ["FOTO_BENCH_LOCAL_DEVICE"])
-    rdv = FileRendezvous(rank, world, timeout=120, dir=os.environ["FOTO_BENCH_RDV_DIR"])
-    with open(os.path.join(os.environ["FOTO_BENCH_PARENT_RDV"], "nccl_id"), "rb") as f:
-        nccl_id = f.read()
+def sharded_step_model(grid, world, nloc):
+    """Per-rank algorithmic HBM bytes of one time-sharded outer iteration: the single-GPU items
+    (STEP_BYTES_PER_VOXEL) on the rank's slab / row box (~nloc Nx Ny voxels each), plus the
+    all-to-all staging -- each of the two slab <-> box all-to-alls reads (W - 1) / W of the slab
+    and writes as much of the box, 8 B each way per voxel -- and the bytes the rank sends over
+    xGMI (16 (W - 1) / W B per slab voxel and outer iteration)."""
+    nx, ny, nt = grid
+    vs = nloc * nx * ny
+    frac = (world - 1) / world
+    items = dict(STEP_BYTES_PER_VOXEL)
+    items["a2a_staging"] = round(32 * frac, 4)
+    per_voxel = sum(items.values())
+    return {"voxels_per_rank": vs, "alg_bytes_per_voxel": round(per_voxel, 4), "items": items,
+            "alg_bytes_per_rank": per_voxel * vs, "xgmi_bytes_per_rank": 16 * frac * vs}
+
+
+class ThreadSync:
+    """FileRendezvous's barrier / max / gather for ranks that are threads of one process
+    (FOTO_BENCH_MOCK_RCCL: every rank over the in-process RCCL transport on one device)."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=300)
+        self.slot = [None] * world
+
+    def abort(self):
+        self.bar.abort()
+
+    def view(self, rank):
+        sync = self
+
+        class View:
+            def barrier(self):
+                sync.bar.wait()
+
+            def gather(self, value):
+                sync.slot[rank] = value
+                sync.bar.wait()
+                out = list(sync.slot)
+                sync.bar.wait()
+                return out
+
+            def max(self, value):
+                return max(self.gather(float(value)))
+
+        return View()
+
+
+def shard_rank(rank, world, device, grid, steps, warmup, cg_mode, nccl_id, sync, timing, library=None):
+    """One rank of the time-sharded solve: its slab of the grid, warmup, a barrier, K timed outer
+    iterations (the slowest rank's clock), then K more with a HIP event pair around every launch
+    (the per-rank kernel table).  Returns rank 0's view with every rank's communicator size and
+    slab length."""
     from foto.bb import BBSolver
     from foto.synthetic import translating_gaussian
-    rho0, rhoT = translating_gaussian(NX, NY)
-    with BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=device, cg_mode=args.cg_mode,
-                  rank=rank, world=world, nccl_id=nccl_id) as t:
-        t.iterate(args.warmup, 0.0, stop_rules=False)
+    nx, ny, nt = grid
+    rho0, rhoT = translating_gaussian(nx, ny)
+    with BBSolver(rho0, rhoT, nt, nx, ny, r=R, reg_epsilon=EPS, device=device, cg_mode=cg_mode, rank=rank,
+                  world=world, nccl_id=nccl_id, library=library) as t:
+        ranks = t.comm_size()
+        t.iterate(warmup, 0.0, stop_rules=False)
         t.sync()
-        rdv.barrier()
+        sync.barrier()
         n0 = len(t.cg_its)
         t0 = time.perf_counter()
-        t.iterate(args.steps, 0.0, stop_rules=False)
+        t.iterate(steps, 0.0, stop_rules=False)
         t.sync()
-        el = rdv.max(time.perf_counter() - t0)
-        rdv.barrier()
+        el = sync.max(time.perf_counter() - t0)
         cg = t.cg_its[n0:]
-    rdv.close()
-    if rank == 0:
-        print(json.dumps({"value": round(args.steps / el, 4), "unit": "iters/s", "ms_per_step": round(1e3 * el / args.steps, 3),
-                          "steps": args.steps, "scaling": "strong", "n_gpus": world,
-                          "cg_iters_per_step": round(float(np.mean(cg)), 2) if cg else None,
-                          "parallelism": f"time-slab x{world}: {NT} planes split over {world} ranks, slab <-> row-box "
-                                         f"all-to-alls and the w_t halo over RCCL (DESIGN.md 5)"}), flush=True)
+        kern = None
+        if timing:
+            t.reset_stats()
+            t.set_timing(True)
+            t.iterate(steps, 0.0, stop_rules=False)
+            t.sync()
+            t.set_timing(False)
+            kern = t.stats()["kernels"]
+        _, nloc = t.shard()
+        info = sync.gather({"rccl_ranks": ranks, "nloc": nloc})
+    return {"elapsed": el, "cg": cg, "kernels": kern, "ranks": info}
 
 
+def shard_summary(res, grid, world, steps, warmup, cg_mode):
+    """Rank 0's object for a time-sharded run: iters/s, every rank's ncclCommCount, the per-rank
+    kernel table, the dominant kernel's roofline and the per-rank step roofline."""
+    el = res["elapsed"]
+    step_s = el / steps
+    rr = [r["rccl_ranks"] for r in res["ranks"]]
+    nloc_max = max(r["nloc"] for r in res["ranks"])
+    out = {"value": round(steps / el, 4), "unit": "iters/s", "ms_per_step": round(1e3 * step_s, 3), "steps": steps,
+           "warmup": warmup, "n_gpus": world, "scaling": "strong", "grid": list(grid),
+           "rccl_ranks": rr[0] if len(set(rr)) == 1 else None, "rccl_ranks_per_rank": rr,
+           "planes_per_rank": [r["nloc"] for r in res["ranks"]],
+           "cg_iters_per_step": round(float(np.mean(res["cg"])), 2) if res["cg"] else None,
+           "model_it_s": MODEL_IT_S.get(tuple(grid), {}).get(world)}
+    kern = res["kernels"]
+    roof = None
+    if kern:
+        out["kernels"] = {name: {"launches": k["n"], "avg_us": round(1e3 * k["ms"] / max(k["n"], 1), 2)}
+                          for name, k in kern.items()}
+        k = kern.get("prox")
+        if k and k["ms"] > 0:
+            avg_s = 1e-3 * k["ms"] / k["n"]
+            ach = (k["bytes"] / k["n"]) / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": "prox", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": k["bytes"] / k["n"],
+                    "avg_launch_us": round(avg_s * 1e6, 2), "note": "rank 0's slab (HIP events, timing pass)"}
+    if cg_mode == 3:
+        m = sharded_step_model(grid, world, nloc_max)
+        ach = m["alg_bytes_per_rank"] / step_s / 1e9
+        m.update({"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                  "xgmi_gbs_per_rank": round(m["xgmi_bytes_per_rank"] / step_s / 1e9, 1),
+                  "note": "per rank: the largest slab's algorithmic bytes over the slowest rank's step time"})
+        if roof is None:
+            roof = {"bound": "hbm", "kernel": None}
+        roof["step"] = m
+    out["roofline"] = roof
+    return out
 
 
-def main():
-    args = parse()
-    if args.cpu_baseline_only:
-        cpu_baseline_child()
-        return
-    if args.gn_cpu_only:
-        gn_cpu_child()
-        return
-    if args.strong_child:
-        strong_child(args)
-        return
+def shard_child(args):
+    """--shard-child: one rank of a time-sharded run (started by run_shard_side with its own
+    rendezvous directory), or, with FOTO_BENCH_MOCK_RCCL=1, every rank as a thread over the
+    in-process RCCL transport on one device (tests)."""
+    world = args.gpus
+    grid = tuple(args.grid)
+    device = int(os.environ.get("FOTO_BENCH_LOCAL_DEVICE", "0"))
+    timing = not args.no_kernel_timing
+    import ctypes
+    from foto import _lib
+    if os.environ.get("FOTO_BENCH_MOCK_RCCL") == "1":
+        import threading
+        L = _lib.load(os.path.join(REPO, "optical-flow-optimal-transport_amd", "foto", "libfoto_mockrccl.so"))
+        buf = ctypes.create_string_buffer(128)
+        _lib.check(L.foto_nccl_unique_id(buf), L)
+        ts = ThreadSync(world)
+        out, errs = [None] * world, []
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # FOTO_BENCH_DEVICES=0,0: rank i on device LIST[i mod len] (tests: two batch-mode ranks on
-    # one GPU); default: the rank's own GPU
-    devs = [int(v) for v in os.environ.get("FOTO_BENCH_DEVICES", "").split(",") if v.strip()]
-    if devs:
-        local_rank = devs[local_rank % len(devs)]
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    rdv = None
-    nccl_id = None
-    sharded = world > 1 and args.mode == "sharded"
-    want_strong = world > 1 and args.mode == "batch" and not args.no_strong
-    if world > 1:
-        rdv = FileRendezvous(rank, world)
-        if sharded or want_strong:
+        def run(g):
+            try:
+                out[g] = shard_rank(g, world, device, grid, args.steps, args.warmup, args.cg_mode, bytes(buf.raw),
+                                    ts.view(g), timing, L)
+            except BaseException as e:  # noqa: BLE001 -- reported below
+                errs.append(f"rank {g}: {e}")
+                ts.abort()
+
+        th = [threading.Thread(target=run, args=(g,)) for g in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise SystemExit("; ".join(sorted(errs))[:600])
+        res = out[0]
+    else:
+        rank = int(os.environ["RANK"])
+        rdv = FileRendezvous(rank, world, timeout=150, dir=os.environ["FOTO_BENCH_RDV_DIR"])
+        try:
             buf = None
             if rank == 0:
-                import ctypes
-                import foto
                 b = ctypes.create_string_buffer(128)
-                foto._lib.check(foto.lib().foto_nccl_unique_id(b))
+                _lib.check(_lib.lib().foto_nccl_unique_id(b))
                 buf = bytes(b.raw)
-            nccl_id = rdv.broadcast("nccl_id", buf)
+            nid = rdv.broadcast("nccl_id", buf)
+            res = shard_rank(rank, world, device, grid, args.steps, args.warmup, args.cg_mode, nid, rdv, timing)
+        except BaseException as e:
+            rdv.abort(str(e))   # (the peers' children stop waiting for this one at once)
+            raise
+        rdv.close()
+        if rank != 0:
+            return
+    print(json.dumps(shard_summary(res, grid, world, args.steps, args.warmup, args.cg_mode)), flush=True)
 
+
+def run_shard_side(args, rdv, rank, world, local_rank, grid, steps, warmup, tag):
+    """A time-sharded run over the N GPUs in child processes (one per rank, `--shard-child`):
+    each rank waits for its child at most FOTO_BENCH_SHARD_TIMEOUT s (default 180) and kills it
+    after that, then every rank's outcome is gathered -- a failure or a hang inside RCCL on ANY
+    rank comes back to rank 0 as (None, error), never as a number.  Returns (result, error) on
+    rank 0, (None, None) elsewhere."""
+    mock = os.environ.get("FOTO_BENCH_MOCK_RCCL") == "1"
+    limit = float(os.environ.get("FOTO_BENCH_SHARD_TIMEOUT", "180"))
+    res, err = None, None
+    if not mock or rank == 0:
+        env = dict(os.environ, FOTO_BENCH_RDV_DIR=os.path.join(rdv.dir, tag), FOTO_BENCH_LOCAL_DEVICE=str(local_rank))
+        cmd = [sys.executable, os.path.abspath(__file__), "--shard-child", "--gpus", str(world), "--steps", str(steps),
+               "--warmup", str(warmup), "--cg-mode", str(args.cg_mode), "--grid", *[str(v) for v in grid]]
+        if args.no_kernel_timing:
+            cmd.append("--no-kernel-timing")
+        proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        try:
+            out, errtxt = proc.communicate(timeout=limit)
+        except subprocess.TimeoutExpired:
+            proc.kill()   # (this rank's own child, by its handle)
+            proc.communicate()
+            err = f"rank {rank}: no result after {limit:.0f} s (killed)"
+        else:
+            if proc.returncode != 0:
+                tail = [ln for ln in (errtxt or "").strip().splitlines() if ln.strip()][-3:]
+                err = f"rank {rank}: exited {proc.returncode}: {' | '.join(tail)}"[:400]
+            elif rank == 0:
+                lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+                res = json.loads(lines[-1]) if lines else None
+                if res is None:
+                    err = "rank 0: no result line"
+    errs = [e for e in rdv.gather(err) if e]
+    if rank != 0:
+        return None, None
+    if errs:
+        return None, "; ".join(errs)[:800]
+    return res, None
+
+
+# ----------------------------------------------------------------------- the solve on this GPU
+
+def measure_local(args, device, rdv):
+    """This GPU's own 640x480x32 solve (N = 1: the headline; N > 1: one of the batch's
+    independent solves): warmup, barrier, K timed steps (max over ranks), then K more with a HIP
+    event pair around every launch (kernel table, dominant kernel's roofline)."""
     from foto.bb import BBSolver
     from foto.synthetic import translating_gaussian
-
     rho0, rhoT = translating_gaussian(NX, NY)
-    # batch mode: this rank's own solve (no RCCL); sharded mode: its slab of the one solve
-    s = BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=local_rank, cg_mode=args.cg_mode,
-                 rank=rank if sharded else 0, world=world if sharded else 1, nccl_id=nccl_id if sharded else None)
-    solves = world if (world > 1 and not sharded) else 1   # problems the timed region advances
+    s = BBSolver(rho0, rhoT, NT, NX, NY, r=R, reg_epsilon=EPS, device=device, cg_mode=args.cg_mode)
 
     def barrier():
         s.sync()
         if rdv is not None:
             rdv.barrier()
 
-    # warmup (untimed)
-    s.iterate(args.warmup, 0.0, stop_rules=False)
+    s.iterate(args.warmup, 0.0, stop_rules=False)   # warmup (untimed)
     barrier()
     s.reset_stats()
     its_before = len(s.cg_its)
@@ -506,10 +655,7 @@ def main():
     cg_steps = s.cg_its[its_before:]
     st_timed = s.stats()
 
-    # per-launch kernel timing pass: K more steps with a HIP event pair around every launch
-    roof = None
-    kern = {}
-    phase_ms = None
+    roof, kern, phase_ms = None, {}, None
     if not args.no_kernel_timing:
         s.reset_stats()
         s.set_timing(True)
@@ -542,82 +688,148 @@ def main():
                     traffic_src = pj.get("_source", "profiles/pmc_traffic.json")
                 except Exception:
                     traffic = None
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": dom, "alg_bytes_per_launch": k["bytes"] / k["n"], "avg_launch_us": round(avg_s * 1e6, 2)}
-            # the same kernel's duration in the timed loop itself (no events between launches), from
-            # the committed rocprofv3 trace of this bench command (tools/prox_segments.py): the
-            # event-bracketed duration above leaves out the hand-over from the previous kernel that
-            # the loop charges to this launch -- both are reported, the loop one is the stricter
+            ev = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 2)}
+            roof = {"bound": "hbm", "achieved": ev["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ev["frac"], "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": dom, "alg_bytes_per_launch": k["bytes"] / k["n"], "avg_launch_us": ev["avg_launch_us"],
+                    "frac_source": "event"}
+            # the headline fraction is the kernel's duration in the timed loop itself (no events
+            # between launches), from the committed rocprofv3 trace of this bench command
+            # (tools/prox_segments.py) when there is one: the event-bracketed duration leaves out
+            # the hand-over from the previous kernel that the loop charges to this launch.  Both
+            # are reported; the loop one is the stricter.
             lt = os.path.join(REPO, "profiles", "prox_loop_trace.json")
             if dom == "prox" and os.path.exists(lt):
                 try:
                     lj = json.load(open(lt))
                     lus = float(lj["loop_avg_us"])
-                    roof["loop_trace"] = {"avg_launch_us": lus,
-                                          "frac": round((k["bytes"] / k["n"]) / (lus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                                          "event_avg_us_same_trace": lj.get("event_avg_us"), "source": lj.get("source")}
+                    lach = (k["bytes"] / k["n"]) / (lus * 1e-6) / 1e9
+                    roof.update({"achieved": round(lach, 1), "frac": round(lach / HBM_PEAK_GBS, 4),
+                                 "avg_launch_us": lus, "frac_source": "loop_trace"})
+                    roof["event_bracketed"] = ev
+                    roof["loop_trace"] = {"avg_launch_us": lus, "event_avg_us_same_trace": lj.get("event_avg_us"),
+                                          "source": lj.get("source")}
                 except Exception:
                     pass
             try:
                 if dom == "spec_cg":
-                    roof.update(stream_ceiling(world if sharded else 1, avg_s * 1e6))
-                elif dom == "prox" and not sharded:
+                    roof.update(stream_ceiling(1, avg_s * 1e6))
+                elif dom == "prox":
                     roof.update(stream_ceiling_prox(avg_s * 1e6))
             except Exception as e:   # an older library in an A/B run (FOTO_LIB) has no probe
                 roof["stream_note"] = f"stream probe unavailable: {e}"
+    s.close()
+    return {"elapsed": elapsed, "cg": cg_steps, "cg_redo": int(st_timed["cg_redo"]), "roofline": roof,
+            "kernels": kern, "phase_ms": phase_ms, "rho0": rho0, "rhoT": rhoT}
 
-    line = None
-    if rank == 0:
-        value = solves * args.steps / elapsed
-        line = {
-            "metric": METRIC,
-            "value": round(value, 4),
-            "unit": "iters/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
+
+def line_base(args, world):
+    return {"metric": METRIC, "value": None, "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+            "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (translating Gaussian pair, SURVEY.md §8(d); no Middlebury offline)",
             "config": {"workload": "FOTO Benamou-Brenier outer iteration, 640x480x32, r=1, eps=1e-2, "
                                    "CG rtol=1e-6 (scipy rule), stop rules off",
-                       "grid": [NX, NY, NT], "cg_mode": ["stencil", "spectral-cg", "spectral-sstep8", "spectral-gauss"][args.cg_mode],
-                       "parallelism": (f"time-slab x{world} (one solve over {world} GPUs, RCCL)" if sharded else
-                                       f"data-parallel x{world} (one solve per GPU, independent pairs as run.py "
-                                       f"streams sequences; 'strong': one solve time-sharded over the {world} GPUs)"
-                                       if world > 1 else "single GPU")},
-            "cg_iters_per_step": round(float(np.mean(cg_steps)), 2) if cg_steps else None,
-            "cg_iters_per_s": round(solves * float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,
-            "phase_ms": phase_ms,
-            "cg_redo": int(st_timed["cg_redo"]),
-            "roofline": roof,
-            "survey_model": {"bytes_per_step": survey_bytes(float(np.mean(cg_steps))) if cg_steps else None,
-                             "equiv_gbs": round(survey_bytes(float(np.mean(cg_steps))) / (elapsed / args.steps) / 1e9, 1)
-                             if cg_steps else None,
-                             "note": "SURVEY.md 8(d) bytes of the literal stencil algorithm, (21 + 10k) N 8 B per "
-                                     "outer iteration, over this run's step time: above HBM peak because the default "
-                                     "path solves the same CG recurrence in the DCT basis (DESIGN.md 3.1)"},
-            "kernels": kern,
-            "epe": None,
-        }
-        if roof is not None:
-            roof["step"] = step_roofline(args.cg_mode, world if sharded else 1, elapsed / args.steps)
-    s.close()
-    if want_strong:   # (child processes: a hang or crash in RCCL is reported, not fatal)
-        strong = strong_side(args, rdv, rank, world, local_rank)
-        if line is not None:
-            line["strong"] = strong
-    if line is not None and world == 1 and args.cg_mode != 0 and not args.no_stencil:
-        line["literal_stencil"] = literal_stencil_rate(rho0, rhoT, local_rank)
+                       "grid": [NX, NY, NT],
+                       "cg_mode": ["stencil", "spectral-cg", "spectral-sstep8", "spectral-gauss"][args.cg_mode],
+                       "parallelism": (f"time-slab x{world}: one 640x480x32 solve sharded on t over {world} GPUs "
+                                       f"(slab <-> row-box all-to-alls, phi / w_t halos, histogram all-gather over "
+                                       f"RCCL; DESIGN.md 5)" if world > 1 else "single GPU")},
+            "epe": None}
+
+
+def main():
+    args = parse()
+    if args.cpu_baseline_only:
+        cpu_baseline_child()
+        return
+    if args.gn_cpu_only:
+        gn_cpu_child()
+        return
+    if args.shard_child:
+        shard_child(args)
+        return
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # FOTO_BENCH_DEVICES=0,0: rank i on device LIST[i mod len] (tests: several ranks on one GPU);
+    # default: the rank's own GPU
+    devs = [int(v) for v in os.environ.get("FOTO_BENCH_DEVICES", "").split(",") if v.strip()]
+    if devs:
+        local_rank = devs[local_rank % len(devs)]
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    if world > 1:
+        rdv = FileRendezvous(rank, world)
+        # 1. the headline: the metric grid time-sharded over the N GPUs
+        shard, err = run_shard_side(args, rdv, rank, world, local_rank, (NX, NY, NT), args.steps, args.warmup, "shard")
+        # 2. config 4 time-sharded over the same GPUs (its own children and communicator)
+        c4 = None
+        if not args.no_c4:
+            c4, c4err = run_shard_side(args, rdv, rank, world, local_rank, C4_GRID, args.c4_steps, args.c4_warmup, "c4")
+            if c4err:
+                c4 = {"value": None, "error": c4err}
+            if c4 is not None:
+                c4["workload"] = "BASELINE config 4: 1024x1024x64 synthetic pair, r=1, eps=1e-2, time-sharded"
+        # 3. the data-parallel side object: one independent solve per GPU, no collective
+        batch = None
+        if not args.no_batch:
+            loc = measure_local(args, local_rank, rdv)
+            if rank == 0:
+                batch = {"value": round(world * args.steps / loc["elapsed"], 4), "unit": "iters/s",
+                         "scaling": "weak", "n_gpus": world,
+                         "ms_per_step": round(1e3 * loc["elapsed"] / args.steps, 3),
+                         "cg_iters_per_step": round(float(np.mean(loc["cg"])), 2) if loc["cg"] else None,
+                         "roofline": loc["roofline"],
+                         "parallelism": f"data-parallel x{world}: one independent 640x480x32 solve per GPU "
+                                        f"(config 5's shape, run.py streams independent sequences); value = "
+                                        f"all {world} solves' outer iterations / the slowest rank's time"}
+        rdv.close()
+        if rank != 0:
+            return
+        line = line_base(args, world)
+        if shard is not None:
+            line.update({"value": shard["value"], "ms_per_step": shard["ms_per_step"],
+                         "rccl_ranks": shard["rccl_ranks"], "cg_iters_per_step": shard["cg_iters_per_step"],
+                         "roofline": shard["roofline"], "sharded": shard})
+        else:
+            line.update({"rccl_ranks": None, "roofline": None, "error": err})
+        line["c4"] = c4
+        line["batch"] = batch
+        print(json.dumps(line))
+        return
+
+    # N = 1
+    loc = measure_local(args, local_rank, None)
+    elapsed, cg_steps = loc["elapsed"], loc["cg"]
+    line = line_base(args, 1)
+    line.update({
+        "value": round(args.steps / elapsed, 4),
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "cg_iters_per_step": round(float(np.mean(cg_steps)), 2) if cg_steps else None,
+        "cg_iters_per_s": round(float(np.sum(cg_steps)) / elapsed, 1) if cg_steps else None,
+        "phase_ms": loc["phase_ms"],
+        "cg_redo": loc["cg_redo"],
+        "roofline": loc["roofline"],
+        "survey_model": {"bytes_per_step": survey_bytes(float(np.mean(cg_steps))) if cg_steps else None,
+                         "equiv_gbs": round(survey_bytes(float(np.mean(cg_steps))) / (elapsed / args.steps) / 1e9, 1)
+                         if cg_steps else None,
+                         "note": "SURVEY.md 8(d) bytes of the literal stencil algorithm, (21 + 10k) N 8 B per "
+                                 "outer iteration, over this run's step time: above HBM peak because the default "
+                                 "path solves the same CG recurrence in the DCT basis (DESIGN.md 3.1)"},
+        "kernels": loc["kernels"],
+    })
+    if line["roofline"] is not None:
+        line["roofline"]["step"] = step_roofline(args.cg_mode, 1, elapsed / args.steps)
+    if args.cg_mode != 0 and not args.no_stencil:
+        line["literal_stencil"] = literal_stencil_rate(loc["rho0"], loc["rhoT"], local_rank)
     # the CPU baselines run after every GPU measurement (no host load beside the timed GPU work),
     # side by side on two cores
     kids = {}
-    gn = gn_side() if (line is not None and world == 1 and not args.no_gn) else None
-    if line is not None and world == 1 and not args.no_cpu_baseline:
+    gn = gn_side() if not args.no_gn else None
+    if not args.no_cpu_baseline:
         kids = start_cpu_children(with_gn=gn is not None)
     if gn is not None:
         gn_cpu = collect_cpu_child(kids, "gn", timeout=1200)
@@ -634,10 +846,7 @@ def main():
                                           f"(CG its {cb['cg_its']}, {cb['loop_s']:.1f} s loop body), "
                                           f"OMP/BLAS threads 1 (single-core path), pinned to one core"}
         line["speedup_vs_cpu"] = round(line["value"] / cpu_value, 1)
-    if rdv is not None:
-        rdv.close()
-    if line is not None:
-        print(json.dumps(line))
+    print(json.dumps(line))
 
 
 if __name__ == "__main__":

@@ -131,7 +131,8 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
  * called from it return the state of the iteration the callback reports (kept intact for a
  * rollback); the one-in-flight loop (sharded, FOTO_PIPE=0) refuses them there with
  * FOTO_ERR_STATE (its next solve overwrites phi).  An error with iterations in flight drains
- * the stream and leaves the context refusing iterate / flow until foto_bb_reset.        */
+ * the stream and leaves the context refusing iterate / flow until foto_bb_reset.
+ * foto_bb_reset and a nested foto_bb_iterate from the callback return FOTO_ERR_STATE.   */
 int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double convergence_tol, int use_stop_rules,
                     foto_bb_iter_cb cb, void* user, int* iters_done);
 /* Flow (u, v, m) from the last phi: utils.opticalflow_from_benamoubrenier.
@@ -147,6 +148,9 @@ int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT);
 int foto_bb_get_phi(foto_bb_ctx* c, double* phi);
 int foto_bb_get_state(foto_bb_ctx* c, double* mu3, double* q3);
 int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc);
+/* Ranks of the context's RCCL communicator (ncclCommCount); 0 for a context without one (one
+ * GPU, or virtual ranks in one process).                                                   */
+int foto_bb_comm_size(const foto_bb_ctx* c, int* nranks);
 int foto_bb_stats_get(const foto_bb_ctx* c, foto_bb_stats* st);
 int foto_bb_stats_reset(foto_bb_ctx* c);
 /* enable / disable per-launch HIP-event timing (foto_bb_stats.n_k / ms_k) */

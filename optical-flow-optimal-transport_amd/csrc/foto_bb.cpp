@@ -207,6 +207,9 @@ struct foto_bb_ctx {
     // an iterate call failed with iterations on the stream: they were drained (drain_inflight),
     // the host state no longer matches the device's, so only foto_bb_reset brings it back
     bool broken = false;
+    // inside foto_bb_iterate (its callback runs with iterations on the stream): reset and a
+    // nested iterate are refused there instead of resetting state under the running loop
+    bool in_iterate = false;
     // bookkeeping
     double prev_crit = -1;
     foto_bb_stats st{};
@@ -1262,8 +1265,11 @@ int foto_bb_iterate(foto_bb_ctx* c, int max_iters, double tol, int use_stop_rule
         set_error("foto_bb_iterate: a previous call failed with outer iterations in flight; foto_bb_reset the context");
         return FOTO_ERR_STATE;
     }
+    if (c->in_iterate) { set_error("foto_bb_iterate: called from its own iteration callback"); return FOTO_ERR_STATE; }
     if (!c->inflight.empty()) { set_error("foto_bb_iterate: an outer iteration is still in flight"); return FOTO_ERR_STATE; }
+    c->in_iterate = true;
     const int rc = iterate_loop(c, max_iters, tol, use_stop_rules, cb, user, iters_done);
+    c->in_iterate = false;
     if (rc < 0) drain_inflight(c);   // (an error leaves no record behind; only a reset continues)
     return rc;
 }
@@ -1346,7 +1352,11 @@ extern "C" {
 
 int foto_bb_reset(foto_bb_ctx* c, const double* rho0, const double* rhoT) {
     if (!c || !rho0 || !rhoT) { set_error("null argument"); return FOTO_ERR_ARG; }
-    drain_inflight(c);   // (normally empty: foto_bb_iterate drains on error)
+    if (c->in_iterate) {   // (from the iteration callback: the loop still owns the in-flight state)
+        set_error("foto_bb_reset: called from foto_bb_iterate's callback");
+        return FOTO_ERR_STATE;
+    }
+    drain_inflight(c);   // (outside foto_bb_iterate nothing is in flight: a no-op unless a call failed)
     c->broken = false;
     const int64_t nxy = (int64_t)c->Nx * c->Ny;
     FOTO_HIP_CHECK(hipStreamSynchronize(c->s));
@@ -1402,6 +1412,13 @@ int foto_bb_shard(const foto_bb_ctx* c, int* t0, int* nloc) {
     if (!c) return FOTO_ERR_ARG;
     if (c->rccl) { *t0 = c->sh[0]->g.t0; *nloc = c->sh[0]->g.nloc; }
     else { *t0 = 0; *nloc = c->Nt; }
+    return 0;
+}
+
+int foto_bb_comm_size(const foto_bb_ctx* c, int* nranks) {
+    if (!c || !nranks) return FOTO_ERR_ARG;
+    *nranks = 0;
+    if (c->rccl && c->nc) FOTO_NCCL_CHECK(ncclCommCount(c->nc, nranks));
     return 0;
 }
 

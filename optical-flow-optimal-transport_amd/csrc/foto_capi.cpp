@@ -346,8 +346,10 @@ static int gn_solve_impl(const double* f1, const double* f2, int w, int h, doubl
         }
         const int rc = foto_gn_plan_solve(cached, f1, f2, u, v, m, iterations);
         if (st && rc >= 0) {
-            double t4[4];
-            FOTO_TRY(foto_gn_plan_timing(cached, t4));
+            // (no early return here: the plan below must still be destroyed when caching is off,
+            // and a timing readback cannot turn a finished solve into an error)
+            double t4[4] = {0, 0, 0, 0};
+            if (foto_gn_plan_timing(cached, t4) < 0) t4[0] = t4[1] = -1.0;
             st->ms_setup = t4[0];
             st->ms_pcg = t4[1];
             st->plan_reused = reused ? 1 : 0;

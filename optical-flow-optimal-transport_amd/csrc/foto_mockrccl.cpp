@@ -148,6 +148,7 @@ const char* ncclGetErrorString(ncclResult_t r) {
         case ncclSystemError: return "mock RCCL: timed out waiting for the peer's matching operation";
         case ncclInvalidUsage: return "mock RCCL: matched send / receive sizes differ";
         case ncclInvalidArgument: return "mock RCCL: invalid argument";
+        case ncclInternalError: return "mock RCCL: communicator refused (FOTO_MOCK_FAIL_INIT)";
         default: return "mock RCCL: HIP error";
     }
 }
@@ -161,6 +162,10 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank) {
     if (!comm || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+    // FOTO_MOCK_FAIL_INIT=1: the communicator is refused (as real RCCL refuses two ranks on one
+    // GPU) -- the failure path of bench.py's sharded headline (tests/test_gpu_bench.py)
+    const char* fi = getenv("FOTO_MOCK_FAIL_INIT");
+    if (fi && atoi(fi) != 0) return ncclInternalError;
     std::lock_guard<std::mutex> lk(g_mu);
     const std::string key(id.internal, strnlen(id.internal, sizeof(id.internal)));
     MockWorld*& w = g_worlds[key];
@@ -173,6 +178,12 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
     if (w->n != nranks) return ncclInvalidArgument;
     w->refs += 1;
     *comm = new ncclComm{w, rank};
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+    if (!comm || !count) return ncclInvalidArgument;
+    *count = comm->w->n;
     return ncclSuccess;
 }
 

@@ -123,6 +123,7 @@ SIGNATURES = {
     "foto_bb_get_phi": (_I, [_P, _D]),
     "foto_bb_get_state": (_I, [_P, _D, _D]),
     "foto_bb_shard": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "foto_bb_comm_size": (_I, [_P, ctypes.POINTER(_I)]),
     "foto_bb_stats_get": (_I, [_P, ctypes.POINTER(BBStats)]),
     "foto_bb_stats_reset": (_I, [_P]),
     "foto_bb_set_timing": (_I, [_P, _I]),

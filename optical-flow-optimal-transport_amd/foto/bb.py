@@ -151,6 +151,12 @@ class BBSolver:
         self._check(self._L.foto_bb_shard(self._ctx, ctypes.byref(t0), ctypes.byref(nl)))
         return t0.value, nl.value
 
+    def comm_size(self):
+        """Ranks of this context's RCCL communicator (ncclCommCount); 0 without one."""
+        n = ctypes.c_int()
+        self._check(self._L.foto_bb_comm_size(self._ctx, ctypes.byref(n)))
+        return n.value
+
     def phi(self):
         _, nl = self.shard()
         out = np.empty(nl * self.Nx * self.Ny)

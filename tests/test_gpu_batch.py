@@ -180,3 +180,31 @@ def test_batch_two_workers_share_one_gpu(tmp_path):
     _, r3, log = _batch(tmp_path, "two", "--seqs=4", "--gpus=2", "--devices=0,0", "--reuse")
     assert log.count("skipped (markers present)") == 4
     assert {s: os.path.getmtime(two / "results" / "synthetic" / s / "foto.flo") for s in seqs} == mt
+
+
+def test_reset_and_nested_iterate_refused_from_callback():
+    """foto_bb_reset (and a nested foto_bb_iterate) from the iteration callback would reset the
+    state the running loop still owns (an iteration in flight, its enqueue count): both are
+    refused with FOTO_ERR_STATE there, and the context keeps iterating to the bits of an
+    untouched run."""
+    from foto import _lib
+    Nt, Nx, Ny, its = 16, 96, 80, 4
+    a0, a1 = _pair(Nx, Ny, 1)
+    with BBSolver(a0, a1, Nt, Nx, Ny, cg_mode=3) as s:
+        ref = _run(s, its)
+    seen = []
+    with BBSolver(a0, a1, Nt, Nx, Ny, cg_mode=3) as s:
+        def cb(i, crit, cg, info):
+            for call in (lambda: s.reset(a0, a1), lambda: s.iterate(1, 0.0, stop_rules=False)):
+                try:
+                    call()
+                    seen.append("accepted")
+                except _lib.FotoError as e:
+                    seen.append(str(e))
+        s.iterate(its, 0.0, stop_rules=False, callback=cb)
+        s.sync()
+        u, v, m = s.flow()
+        got = dict(u=u, v=v, m=m, phi=s.phi(), crit=np.array(s.crit[:its]), cg=np.array(s.cg_its[:its]))
+    assert len(seen) == 2 * its and all("callback" in e for e in seen), seen
+    for k in ("u", "v", "m", "phi", "crit", "cg"):
+        assert np.array_equal(got[k], ref[k]), k

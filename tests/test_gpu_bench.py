@@ -44,56 +44,73 @@ def test_bench_json_line():
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None
 
 
-def test_bench_two_ranks_batch_mode_one_gpu(tmp_path):
-    """bench.py --gpus 2 as the driver launches it (torch.distributed.run, one process per rank,
-    the file rendezvous), both ranks on this one GPU (FOTO_BENCH_DEVICES=0,0): the default batch
-    mode -- one 640x480x32 solve per rank, value = both solves' outer iterations per second on the
-    slowest rank's clock, "scaling": "weak".  (The time-sharded side run needs two GPUs for RCCL:
-    --no-strong here; its call sequences are checked by tests/test_gpu_rccl_mock.py.)"""
-    # (the two ranks started here the way torch.distributed.run starts them -- children of one
-    # process, RANK / WORLD_SIZE / LOCAL_RANK / MASTER_PORT set -- without its torch import)
+def _ranks(n, port, extra_env=None, args=()):
+    """bench.py --gpus n as the driver launches it (torch.distributed.run: one process per rank,
+    RANK / WORLD_SIZE / LOCAL_RANK / MASTER_PORT set, children of one process) without its torch
+    import, every rank on this one GPU (FOTO_BENCH_DEVICES=0) and the time-sharded runs over the
+    in-process RCCL transport (FOTO_BENCH_MOCK_RCCL=1: rank 0's child runs the n ranks as threads
+    over libfoto_mockrccl.so -- real RCCL refuses two ranks on one device).  Returns rank 0's line."""
     procs = []
-    for g in range(2):
-        env = dict(os.environ, FOTO_BENCH_DEVICES="0,0", WORLD_SIZE="2", RANK=str(g), LOCAL_RANK=str(g),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT="29617")
-        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-               "--no-cpu-baseline", "--no-gn", "--no-stencil", "--no-strong"]
+    for g in range(n):
+        env = dict(os.environ, FOTO_BENCH_DEVICES="0", FOTO_BENCH_MOCK_RCCL="1", WORLD_SIZE=str(n), RANK=str(g),
+                   LOCAL_RANK=str(g), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   FOTO_BENCH_SHARD_TIMEOUT="150", **(extra_env or {}))
+        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline", "--no-gn", "--no-stencil", *args]
         procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True))
-    outs = [p.communicate(timeout=240) for p in procs]
+    outs = [p.communicate(timeout=280) for p in procs]
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
     lines = [ln for o, _ in outs for ln in o.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, [o[-1000:] for o, _ in outs]   # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 3
-    assert "data-parallel x2" in d["config"]["parallelism"]
-    # two problems advanced in the timed region: value = 2 K / elapsed
-    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 2.0) < 0.02
+    print({k: d.get(k) for k in ("value", "ms_per_step", "rccl_ranks", "error")},
+          {k: (d[k] or {}).get("value") if isinstance(d.get(k), dict) else None for k in ("batch", "c4")})
+    return d
+
+
+def _check_strong(d, n):
+    assert d["n_gpus"] == n and d["scaling"] == "strong" and d["steps"] == 3
+    assert d["rccl_ranks"] == n   # ncclCommCount of every rank's communicator
+    assert "time-slab x%d" % n in d["config"]["parallelism"]
+    assert d["value"] > 0 and abs(d["value"] * d["ms_per_step"] / 1e3 - 1.0) < 0.01
     assert 150 <= d["cg_iters_per_step"] <= 210
-    assert "strong" not in d
+    sh = d["sharded"]
+    assert sum(sh["planes_per_rank"]) == 32 and sh["rccl_ranks_per_rank"] == [n] * n
+    st = d["roofline"]["step"]
+    assert st["items"]["a2a_staging"] == round(32 * (n - 1) / n, 4)
+    assert st["alg_bytes_per_rank"] == st["alg_bytes_per_voxel"] * st["voxels_per_rank"]
+    assert d["roofline"]["kernel"] == "prox" and d["roofline"]["frac"] > 0
+    assert sh["model_it_s"] == {2: 886, 4: 1729, 8: 2317}.get(n)
+    b = d["batch"]   # the data-parallel number: a labelled side object, never the headline
+    assert b["scaling"] == "weak" and b["n_gpus"] == n and abs(b["value"] * b["ms_per_step"] / 1e3 - n) < 0.02 * n
 
 
-def test_bench_strong_side_run_failure_is_reported(tmp_path):
-    """The batch mode's time-sharded side run runs in a child process per rank: here, with both
-    ranks on one GPU, RCCL refuses the communicator (one device for two ranks), and the children
-    fail -- the headline line must still come out of rank 0 with the failure reported in
-    "strong", and both ranks must exit 0 (a crash or hang inside RCCL on the driver's 8-GPU node
-    cannot cost the data-parallel measurement)."""
-    procs = []
-    for g in range(2):
-        env = dict(os.environ, FOTO_BENCH_DEVICES="0,0", WORLD_SIZE="2", RANK=str(g), LOCAL_RANK=str(g),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT="29619", FOTO_BENCH_STRONG_TIMEOUT="90")
-        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-               "--no-cpu-baseline", "--no-gn", "--no-stencil"]
-        procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                      text=True))
-    outs = [p.communicate(timeout=300) for p in procs]
-    for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e[-3000:]
-    lines = [ln for o, _ in outs for ln in o.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, [o[-1000:] for o, _ in outs]
-    d = json.loads(lines[0])
-    print("strong:", d.get("strong"))
-    assert d["scaling"] == "weak" and d["n_gpus"] == 2
-    assert "strong" in d and ("error" in d["strong"] or "value" in d["strong"])
+def test_bench_n2_line_time_sharded_headline():
+    """N = 2: value = the one 640x480x32 solve time-sharded over the two ranks (RCCL branches),
+    "scaling": "strong", rccl_ranks 2; config 4 (1024x1024x64) sharded the same way in "c4";
+    the independent-solve throughput only in "batch"."""
+    d = _ranks(2, 29617, args=("--c4-steps", "1", "--c4-warmup", "1"))
+    _check_strong(d, 2)
+    c4 = d["c4"]
+    assert c4["value"] > 0 and c4["grid"] == [1024, 1024, 64] and c4["rccl_ranks"] == 2, c4
+    assert c4["planes_per_rank"] == [32, 32]
+
+
+def test_bench_n8_line_time_sharded_headline():
+    """N = 8 (the driver's scaling node): four planes per rank, rccl_ranks 8."""
+    d = _ranks(8, 29618, args=("--no-c4",))
+    _check_strong(d, 8)
+    assert d["sharded"]["planes_per_rank"] == [4] * 8
+    assert d["c4"] is None
+
+
+def test_bench_rccl_failure_gives_null_value():
+    """An RCCL failure (the mock refuses the communicator, as real RCCL refuses two ranks on one
+    GPU): the headline value is null with the error in the line -- the batch number, which
+    needs no collective, is still measured but stays in "batch" -- and every rank exits 0."""
+    d = _ranks(2, 29619, extra_env={"FOTO_MOCK_FAIL_INIT": "1"}, args=("--no-c4",))
+    assert d["value"] is None and d["ms_per_step"] is None and d["rccl_ranks"] is None
+    assert "ncclCommInitRank" in d["error"] or "refused" in d["error"], d["error"]
+    assert d["scaling"] == "strong" and d["batch"]["value"] > 0

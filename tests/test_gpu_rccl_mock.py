@@ -178,7 +178,12 @@ def test_rccl_comm_stream_pipelined_alltoall_and_phi_halo(monkeypatch, W):
     monkeypatch.setenv("FOTO_A2A_HALO", "0")
     monkeypatch.setenv("FOTO_COMM_STREAM", "0")
     plain = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
-    for env in ({}, {"FOTO_A2A_PARTS": "3"}, {"FOTO_A2A_HALO": "0"}, {"FOTO_COMM_STREAM": "0"}):
+    # (at 48 x 40 the halo delivery is off by default -- a2a_big_planes -- so it is forced on here:
+    # alltoall_part_xfers with halo = 1, the inverse DCTs on nloc + 2 planes, prox without its
+    # own phi halo exchange)
+    for env in ({}, {"FOTO_A2A_PARTS": "3"}, {"FOTO_A2A_HALO": "0"}, {"FOTO_COMM_STREAM": "0"},
+                {"FOTO_A2A_HALO": "1"}, {"FOTO_A2A_PARTS": "3", "FOTO_A2A_HALO": "1"},
+                {"FOTO_A2A_PARTS": "2", "FOTO_A2A_HALO": "1", "FOTO_COMM_STREAM": "0"}):
         for k in ("FOTO_A2A_PARTS", "FOTO_A2A_HALO", "FOTO_COMM_STREAM", "FOTO_WT_OVERLAP"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
@@ -215,8 +220,13 @@ def test_rccl_wt_exchange_overlapped_with_interior_planes(monkeypatch, W, parts)
     compare(ranks, virt, Nt, Nx, Ny, W)
     monkeypatch.setenv("FOTO_WT_PRE", "1")   # virtual ranks with k_wt_pre (tools/proxy_scaling.py)
     compare(ranks, run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3), Nt, Nx, Ny, W)
-    for a, b in zip(ranks, seq):
-        assert a["crit"] == b["crit"] and a["cg"] == b["cg"]
-        np.testing.assert_array_equal(a["phi"], b["phi"])
-    for a, b in zip(ranks[0]["flow"], seq[0]["flow"]):
-        np.testing.assert_array_equal(a, b)
+    monkeypatch.delenv("FOTO_WT_PRE")
+    # k_wt_pre reads the phi halo plane: with the halo delivered inside the backward all-to-all too
+    monkeypatch.setenv("FOTO_A2A_HALO", "1")
+    halo = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=4, cg_mode=3)
+    for got in (ranks, halo):
+        for a, b in zip(got, seq):
+            assert a["crit"] == b["crit"] and a["cg"] == b["cg"]
+            np.testing.assert_array_equal(a["phi"], b["phi"])
+        for a, b in zip(got[0]["flow"], seq[0]["flow"]):
+            np.testing.assert_array_equal(a, b)

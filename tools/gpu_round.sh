@@ -1,10 +1,9 @@
 #!/bin/bash
-# round-5 GPU check: the whole -m gpu suite, smoke, one default bench line (no CPU baselines)
+# A round's GPU check: the whole -m gpu suite (prints kept), smoke, one default bench line
+# without the CPU baselines.  tools/gpu_round.sh TAG   (from the repo root on the GPU box)
 set -o pipefail
-O=gpurun_out
-tag="${1:-r05}"
-mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -s --timeout 200 --timeout-method thread -p no:cacheprovider > $O/tests_$tag.log 2>&1
+O=gpurun_out; tag="${1:-r06}"; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 200 --timeout-method thread -p no:cacheprovider > $O/tests_$tag.log 2>&1
 rc=$?
 echo "tests rc=$rc"; tail -3 $O/tests_$tag.log; grep -E "^FAILED|^ERROR" $O/tests_$tag.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
