@@ -81,8 +81,9 @@ typedef struct {
                           /* eigenbasis, one pass / iteration), 2 = spectral s-step CG     */
                           /* (one pass / up to 8 iterations, any world; mode 1 needs       */
                           /* world == 1; eps <= 0 selects mode 0), 3 = spectral CG on the  */
-                          /* Gauss-compressed measure of b^ (default: one read of b^, the  */
-                          /* recurrence on 2048 nodes, any world)                          */
+                          /* Gauss-compressed measure of b^ (one read of b^, the           */
+                          /* recurrence on 2048 nodes, any world); < 0 = auto (default):   */
+                          /* 0 on grids of <= 2^18 voxels (FOTO_CG_AUTO_MAX), 3 above      */
     int rank, world;      /* time-slab sharding over `world` processes (RCCL); 1 = single  */
     const void* nccl_id;  /* 128-byte ncclUniqueId (foto_nccl_unique_id on rank 0)         */
     int virtual_ranks;    /* >1: shard over this many in-process slabs on ONE device       */

