@@ -762,6 +762,9 @@ hipError_t launch_q_from_phi(const Geo& g, const double* phi, const double* mut,
 #endif
 // 1: tiles whose phi region lies inside the plane run a copy of the march without bound tests
 // (prox_rhs_body<.., true>); 0: every tile runs the general one (A/B builds)
+#ifndef FOTO_PR_CHFAST
+#define FOTO_PR_CHFAST 0   // 1: block order tile-major with the chunks fastest (A/B builds)
+#endif
 #ifndef FOTO_PR_INTERIOR
 #define FOTO_PR_INTERIOR 1
 #endif
@@ -1046,7 +1049,13 @@ __global__ __launch_bounds__(PR_NT) __attribute__((amdgpu_waves_per_eu(PR_WPE)))
     const int Nx = g.Nx, Ny = g.Ny;
     const int ntx = (Nx + PR_X - 1) / PR_X, ntiles = ntx * ((Ny + PR_Y - 1) / PR_Y);
     const int lin = xcd_tile(blockIdx.x);
+#if FOTO_PR_CHFAST
+    // a tile's chunks adjacent in the block order (one XCD, resident together)
+    const int nch = (g.nloc + tch - 1) / tch;
+    const int tile = lin / nch, ch = lin - tile * nch;
+#else
     const int ch = lin / ntiles, tile = lin - ch * ntiles;
+#endif
     const int x0 = (tile % ntx) * PR_X, y0 = (tile / ntx) * PR_Y;
     double num, den, ff;
 #if FOTO_PR_INTERIOR

@@ -3203,6 +3203,8 @@ struct SpecImpl {
     double* gq_tab = nullptr;
     GqBins* gq_bins = nullptr;    // bin edges of the measure and the solution table
     GqQCos* gq_qcos = nullptr;    // the solution table's transform constants
+    GqPub* gq_pub = nullptr;      // k_gq_cgtab's (alpha, beta) slots
+    bool gq_cgtab = true;         // FOTO_GQ_CGTAB=0: k_gq_cg, then k_gq_qtab
     // bin-ordered histogram (k_gq_hist_perm): the box's voxels grouped by bin, chunked
     unsigned* gq_permv = nullptr;
     GqChunk* gq_chunks = nullptr;
@@ -3238,6 +3240,7 @@ struct SpecImpl {
     bool vec() const { return (g.Nx % 2) == 0; }
     double nbox() const { return (double)g.Nt * nyl * g.Nx; }
 };
+static int gq_pub_clear(SpecImpl* P, hipStream_t s);
 
 // orthonormal DCT-II matrix C[k][j] = s_k cos(pi k (2j+1) / (2n)) (long double on the host)
 // eigenvalues 2 - 2 cos(pi k / n) of the Neumann second difference (the same values dct_matrix gives)
@@ -3452,6 +3455,10 @@ int SpectralPlan::init(const Geo& g, int rank, int world, double r, double eps, 
         k_gq_bins<<<1, 256, 0, s>>>(P->gq_bins);
         FOTO_TRY(P->alloc(sizeof(GqQCos), &b)); P->gq_qcos = (GqQCos*)b;
         k_gq_qcos<<<1, 256, 0, s>>>(P->gq_qcos);
+        FOTO_TRY(P->alloc(sizeof(GqPub), &b)); P->gq_pub = (GqPub*)b;
+        FOTO_TRY(gq_pub_clear(P, s));
+        const char* ct = getenv("FOTO_GQ_CGTAB");
+        P->gq_cgtab = !(ct && atoi(ct) == 0);
         FOTO_HIP_CHECK(hipGetLastError());
         FOTO_TRY(P->alloc(sizeof(GqExact), &b)); P->gq_exact = (GqExact*)b;
         FOTO_TRY(gq_build_perm(P, s));
@@ -3875,6 +3882,14 @@ static int gq_measure(SpecImpl* P, KTimer* kt, hipStream_t s) {
     return 0;
 }
 
+// k_gq_cgtab's slots as a fresh plan has them: every (alpha, beta) NaN, kdone -1, ticket 0
+static int gq_pub_clear(SpecImpl* P, hipStream_t s) {
+    if (!P->gq_pub) return 0;
+    FOTO_HIP_CHECK(hipMemsetAsync(P->gq_pub, 0xff, sizeof(GqPub), s));   // (all-ones: NaN, -1)
+    FOTO_HIP_CHECK(hipMemsetAsync(&P->gq_pub->ticket, 0, sizeof(unsigned), s));
+    return 0;
+}
+
 // the world histograms -> Gauss nodes -> CG coefficients -> solution table; header to host
 static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream_t s) {
     hipEvent_t e = kt ? kt->start(s) : nullptr;
@@ -3894,10 +3909,17 @@ static int gq_solve(SpecImpl* P, double rtol, int maxiter, KTimer* kt, hipStream
     P->hslot ^= 1;
     const char* hc = getenv("FOTO_HOST_CRIT");
     const bool direct = !(hc && atoi(hc) == 0);
-    k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq, direct ? P->dgq2[P->hlast] : nullptr);
-    FOTO_HIP_CHECK(hipGetLastError());
-    k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->gq_qcos, P->r * P->eps, P->c1, P->gq_tab);
-    FOTO_HIP_CHECK(hipGetLastError());
+    if (P->gq_cgtab) {
+        k_gq_cgtab<<<1 + GQ_TAB / 256, 256, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq,
+                                                    direct ? P->dgq2[P->hlast] : nullptr, P->gq_pub, P->gq_bins,
+                                                    P->gq_qcos, P->r * P->eps, P->c1, P->gq_tab);
+        FOTO_HIP_CHECK(hipGetLastError());
+    } else {
+        k_gq_cg<<<1, GQ_CGNTH, 0, s>>>(P->gqn, rtol, maxiter, klim, P->gq, direct ? P->dgq2[P->hlast] : nullptr);
+        FOTO_HIP_CHECK(hipGetLastError());
+        k_gq_qtab<<<GQ_TAB / 256, 256, 0, s>>>(P->gq, P->gq_bins, P->gq_qcos, P->r * P->eps, P->c1, P->gq_tab);
+        FOTO_HIP_CHECK(hipGetLastError());
+    }
     if (kt) kt->stop(e, s, FOTO_K_SPEC, 0.0);
     if (!direct)
         FOTO_HIP_CHECK(hipMemcpyAsync(P->hgq2[P->hlast], P->gq, offsetof(GqState, alpha), hipMemcpyDeviceToHost, s));
@@ -4303,6 +4325,7 @@ int SpectralPlan::reset(hipStream_t s) {
     P->npend = 0;
     P->gauss_active = false;
     if (P->gq) FOTO_HIP_CHECK(hipMemsetAsync(P->gq, 0, sizeof(GqState), s));
+    FOTO_TRY(gq_pub_clear(P, s));
     P->last_passes = 0;
     FOTO_HIP_CHECK(hipMemsetAsync(P->S, 0, sizeof(CGScal), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->rb.ticket, 0, 8 * sizeof(double), s));

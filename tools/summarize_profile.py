@@ -26,7 +26,7 @@ SHORT = {
     "k_cg_upd": "cg_upd", "k_cg_dir": "cg_dir", "k_prox_rhs": "prox", "k_prox": "prox_sep", "k_rhs": "rhs",
     "k_gq_hist": "gq_hist", "k_gq_reduce": "gq_reduce", "k_gq_perm_reduce": "gq_reduce",
     "k_gq_perm_count": "gq_setup", "k_gq_perm_fill": "gq_setup", "k_gq_perm_scan": "gq_setup",
-    "k_gq_exact": "gq_setup", "k_gq_rowmu": "gq_setup", "k_gq_bins": "gq_setup", "k_gq_nodes": "gq_nodes", "k_gq_cg": "gq_cg",
+    "k_gq_exact": "gq_setup", "k_gq_rowmu": "gq_setup", "k_gq_bins": "gq_setup", "k_gq_nodes": "gq_nodes", "k_gq_cgtab": "gq_cg", "k_gq_cg": "gq_cg",
     "k_gq_qtab": "gq_qtab", "k_gq_xhat": "gq_xhat", "k_dct_t_inv_q": "dct_t_q", "k_dct_tp_inv_q": "dct_tp_q",
     "k_dct_tp_fwd_init": "dct_tp_init", "k_dct_tp_inv_xhat": "dct_tp_xhat",
     "k_spec_s2_plan": "spec_plan", "k_spec_s2": "spec_cg", "k_spec_init": "spec_init", "k_spec_xhat": "spec_xhat",
