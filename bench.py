@@ -597,6 +597,9 @@ def run_shard_side(args, rdv, rank, world, local_rank, grid, steps, warmup, tag)
     res, err = None, None
     if not mock or rank == 0:
         env = dict(os.environ, FOTO_BENCH_RDV_DIR=os.path.join(rdv.dir, tag), FOTO_BENCH_LOCAL_DEVICE=str(local_rank))
+        # RCCL's bootstrap over loopback: the ranks share one node, and the container's hostname
+        # or default interface may not resolve (the intra-node transports are P2P / SHM either way)
+        env.setdefault("NCCL_SOCKET_IFNAME", "lo")
         cmd = [sys.executable, os.path.abspath(__file__), "--shard-child", "--gpus", str(world), "--steps", str(steps),
                "--warmup", str(warmup), "--cg-mode", str(args.cg_mode), "--grid", *[str(v) for v in grid]]
         if args.no_kernel_timing:
@@ -723,6 +726,19 @@ def measure_local(args, device, rdv):
             "kernels": kern, "phase_ms": phase_ms, "rho0": rho0, "rhoT": rhoT}
 
 
+def visible_device(local_rank):
+    """The HIP ordinal of this rank's GPU: LOCAL_RANK, unless the launcher narrowed the visible
+    devices (HIP_ / ROCR_ / CUDA_VISIBLE_DEVICES listing fewer than LOCAL_RANK + 1 of them, e.g.
+    one per process) -- then the rank's GPU is the one it can see."""
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(k)
+        if v is not None and v.strip():
+            n = len([d for d in v.split(",") if d.strip()])
+            if 0 < n <= local_rank:
+                return local_rank % n
+    return local_rank
+
+
 def line_base(args, world):
     return {"metric": METRIC, "value": None, "unit": "iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
@@ -758,6 +774,8 @@ def main():
     devs = [int(v) for v in os.environ.get("FOTO_BENCH_DEVICES", "").split(",") if v.strip()]
     if devs:
         local_rank = devs[local_rank % len(devs)]
+    else:
+        local_rank = visible_device(local_rank)
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 

@@ -88,3 +88,13 @@ def test_n2_line_without_a_device_reports_null_value(tmp_path):
     assert d["value"] is None and d["scaling"] == "strong" and d["n_gpus"] == 2 and d["rccl_ranks"] is None
     assert "rank 0" in d["error"] and "rank 1" in d["error"], d["error"]
     assert d["batch"] is None and d["c4"] is None
+
+
+def test_visible_device(bench, monkeypatch):
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    assert bench.visible_device(5) == 5                  # every GPU visible: LOCAL_RANK
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")       # one GPU per process
+    assert bench.visible_device(5) == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    assert bench.visible_device(5) == 5
