@@ -645,6 +645,15 @@ __device__ __forceinline__ V ld_dead(const V* p) {
 
 // Strided (y-axis) lines get a slightly larger LDS budget: at N = 1024 a line image is 8448 B,
 // so 64 KB held 4 lines (32-B row segments) and 68 KB holds 8 (64 B; still two blocks per CU)
+#ifndef FOTO_FFT_LINE_THREADS
+#define FOTO_FFT_LINE_THREADS 1   // contiguous lines: output rounds per thread group of one line (0: flat idx rounds)
+#endif
+#ifndef FOTO_FFT_TW_PT
+#define FOTO_FFT_TW_PT 0       // 1: stage-1 twiddles from the LDS post-twiddle table (PT_LDS kernels; measured no faster)
+#endif
+#ifndef FOTO_FFT_PT_LDS
+#define FOTO_FFT_PT_LDS 1      // 0: the pre / post twiddles read from the global table per element
+#endif
 #ifndef FOTO_FFT_STRIDED_LDS
 #define FOTO_FFT_STRIDED_LDS 69632
 #endif
@@ -665,7 +674,29 @@ struct FftGeom {
     }
     static constexpr int LPB = lpb();
     static constexpr int TAB = 6 * M + 6;
+    // the output / input phase twiddles (PA, PB of the table: 4 doubles per k = 0 .. M) staged in
+    // LDS when that keeps the blocks per CU the LDS allows (x at 640: 3 of 43 + 10 KB; y at 480: 2
+    // of 65 + 8 KB; not y at 1024, whose 8 lines already take 66 KB)
+    static constexpr int PTN = 4 * (M + 1);
+    static constexpr int LDS_B = LPB * LS * 8 + 16;
+    static constexpr bool PT_LDS = FOTO_FFT_PT_LDS && (163840 / (LDS_B + 8 * PTN)) == (163840 / LDS_B);
 };
+
+// PT[4k .. 4k + 3] = (PA_k, PB_k): e^{-2 pi i k / N}, e^{-i pi k / (2N)}
+template <class G>
+__device__ __forceinline__ void fft_pt_fill(double* PT, const double* __restrict__ tab) {
+    if constexpr (G::PT_LDS) {
+        const double* PA = tab + 2 * G::M;
+        const double* PB = PA + 2 * (G::M + 1);
+        for (int p = threadIdx.x; p < G::M + 1; p += blockDim.x) {
+            const double a0 = PA[2 * p], a1 = PA[2 * p + 1], b0 = PB[2 * p], b1 = PB[2 * p + 1];
+            PT[4 * p] = a0;
+            PT[4 * p + 1] = a1;
+            PT[4 * p + 2] = b0;
+            PT[4 * p + 3] = b1;
+        }
+    }
+}
 
 template <int M2>
 __device__ __forceinline__ int fft_zpos(int j) { return j + j / M2; }   // natural index -> LDS complex position
@@ -790,9 +821,13 @@ __device__ __forceinline__ void dft_reg(double (&xr)[R], double (&xi)[R]) {
 
 // stage 1 (in place on the LDS lines): for each (line, j2): the length-M1 DFT of
 // z[M2 j1 + j2] (dft_reg), times e^{-+2 pi i j2 k1 / M}, stored at row k1, column j2
-template <int M1, int M2, bool INV, int LPB, int NTH = 256>
-__device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
+// PT (TWPT, round 6): the twiddles from the LDS copy of the post-twiddle table instead of the
+// global table: e^{-2 pi i q / M} = PA_{2q} for 2q <= M (the same bits: the table's long-double
+// angle 2 pi (2q) / (2M) is 2 pi q / M exactly), conj PA_{2(M-q)} above (within an ulp)
+template <int M1, int M2, bool INV, int LPB, int NTH = 256, bool TWPT = false>
+__device__ __forceinline__ void fft_stage1(double* L, const double* TW, const double* PT = nullptr) {
     constexpr int LS = FftGeom<M1, M2>::LS;
+    constexpr int M = M1 * M2;
     for (int task = threadIdx.x; task < LPB * M2; task += NTH) {
         const int l = task / M2, j2 = task - (task / M2) * M2;
         double* Ll = L + l * LS;
@@ -806,7 +841,16 @@ __device__ __forceinline__ void fft_stage1(double* L, const double* TW) {
 #pragma unroll
         for (int k1 = 0; k1 < M1; ++k1) {
             const int q = j2 * k1;   // < M
-            const double tr = TW[2 * q], ti = INV ? -TW[2 * q + 1] : TW[2 * q + 1];
+            double tr, ti;
+            if constexpr (TWPT) {
+                const bool lo = 2 * q <= M;
+                const dbl2 w = *reinterpret_cast<const dbl2*>(&PT[8 * (lo ? q : M - q)]);
+                tr = w.x;
+                ti = (lo != INV) ? w.y : -w.y;
+            } else {
+                tr = TW[2 * q];
+                ti = INV ? -TW[2 * q + 1] : TW[2 * q + 1];
+            }
             Ll[2 * ((M2 + 1) * k1 + j2)] = fma(xr[k1], tr, -xi[k1] * ti);
             Ll[2 * ((M2 + 1) * k1 + j2) + 1] = fma(xr[k1], ti, xi[k1] * tr);
         }
@@ -1006,6 +1050,7 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_fwd(int outer, int inner, const
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
     __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
+    __shared__ __attribute__((aligned(16))) double PT[G::PT_LDS ? G::PTN : 2];
 #if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
 #else
@@ -1015,6 +1060,7 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_fwd(int outer, int inner, const
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     if constexpr (LdsPrime<M2>::value)
         for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
+    fft_pt_fill<G>(PT, tab);
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
@@ -1024,55 +1070,89 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_fwd(int outer, int inner, const
 #endif
     {   // load (all rounds' loads in flight), then store in Makhoul order
         using RD = FftRounds<LPB * N, NTH>;
+        // element j0 of this thread: (line l, position j); contiguous lines by line thread groups
+        // (round 6: no index division per element)
+        constexpr bool LT = CONTIG && FOTO_FFT_LINE_THREADS && NTH % LPB == 0 && N % (NTH / LPB) == 0 &&
+                            N / (NTH / LPB) == RD::R;
+        auto lj = [&](int j0, int& l, int& j) -> bool {
+            if constexpr (LT) {
+                l = tid / (NTH / LPB);
+                j = tid - l * (NTH / LPB) + (NTH / LPB) * j0;
+                return true;
+            } else {
+                const int idx = tid + NTH * j0;
+                if (CONTIG) { l = idx / N; j = idx - l * N; }
+                else { j = idx / LPB; l = idx - j * LPB; }
+                return RD::ok(idx);
+            }
+        };
         double xv[RD::R];
 #pragma unroll
         for (int j0 = 0; j0 < RD::R; ++j0) {
-            const int idx = tid + NTH * j0;
             int l, j;
-            if (CONTIG) { l = idx / N; j = idx - l * N; }
-            else { j = idx / LPB; l = idx - j * LPB; }
-            xv[j0] = (RD::ok(idx) && l < f.nl) ? ld_dead(&in[base(l) + j * st]) : 0.0;
+            const bool ok = lj(j0, l, j);
+            xv[j0] = (ok && l < f.nl) ? ld_dead(&in[base(l) + j * st]) : 0.0;
         }
 #pragma unroll
         for (int j0 = 0; j0 < RD::R; ++j0) {
-            const int idx = tid + NTH * j0;
-            if (!RD::ok(idx)) continue;
             int l, j;
-            if (CONTIG) { l = idx / N; j = idx - l * N; }
-            else { j = idx / LPB; l = idx - j * LPB; }
+            if (!lj(j0, l, j)) continue;
             const int p = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
             L[l * LS + 2 * fft_zpos<M2>(p >> 1) + (p & 1)] = xv[j0];
         }
     }
     __syncthreads();
-    fft_stage1<M1, M2, false, LPB, NTH>(L, TW);
+    fft_stage1<M1, M2, false, LPB, NTH, G::PT_LDS && FOTO_FFT_TW_PT>(L, TW, PT);
     __syncthreads();
     fft_stage2_any<M1, M2, false, LPB, NTH>(L, CS);
     __syncthreads();
     const double* PA = tab + 2 * M;
     const double* PB = PA + 2 * (M + 1);
     const double s0 = PB[2 * (M + 1)], s = PB[2 * (M + 1) + 1];
-    using RO = FftRounds<LPB * (M + 1), NTH>;
-#pragma unroll
-    for (int j0 = 0; j0 < RO::R; ++j0) {
-        const int idx = tid + NTH * j0;
-        if (!RO::ok(idx)) continue;
-        int l, k;
-        if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
-        else { k = idx / LPB; l = idx - k * LPB; }
-        if (l >= f.nl) continue;
+    auto emit = [&](int l, int k) {   // X_k and X_{N-k} of line l
         const double* Ll = L + l * LS;
         const int pa = 2 * fft_pos<M1, M2>(k == M ? 0 : k), pb = 2 * fft_pos<M1, M2>(k == 0 ? 0 : M - k);
         const double zr = Ll[pa], zi = Ll[pa + 1], cr = Ll[pb], ci = -Ll[pb + 1];
         const double er = 0.5 * (zr + cr), ei = 0.5 * (zi + ci);     // DFT of the even samples
         const double orr = 0.5 * (zi - ci), oi = 0.5 * (cr - zr);     // DFT of the odd samples
-        const double war = PA[2 * k], wai = PA[2 * k + 1];
+        double war, wai, wbr, wbi;
+        if constexpr (G::PT_LDS) {
+            const dbl2 a = *reinterpret_cast<const dbl2*>(&PT[4 * k]), b = *reinterpret_cast<const dbl2*>(&PT[4 * k + 2]);
+            war = a.x; wai = a.y; wbr = b.x; wbi = b.y;
+        } else {
+            war = PA[2 * k]; wai = PA[2 * k + 1]; wbr = PB[2 * k]; wbi = PB[2 * k + 1];
+        }
         const double vr = er + fma(war, orr, -wai * oi), vi = ei + fma(war, oi, wai * orr);
-        const double wbr = PB[2 * k], wbi = PB[2 * k + 1];
         const double yr = fma(wbr, vr, -wbi * vi), yi = fma(wbr, vi, wbi * vr);
         const int64_t b = base(l);
         out[b + k * st] = (k == 0 ? s0 : s) * yr;
         if (k > 0 && k < M) out[b + (N - k) * st] = -s * yi;
+    };
+    if constexpr (CONTIG && FOTO_FFT_LINE_THREADS && NTH % LPB == 0) {
+        // (round 6) a fixed line per thread group of NTH / LPB threads, k = t, t + TPL, ...: no
+        // index division per element, and the line test hoisted out of the rounds
+        constexpr int TPL = NTH / LPB, RK = (M + 1 + TPL - 1) / TPL;
+        const int l = tid / TPL, t = tid - l * TPL;
+        if (l < f.nl) {
+#pragma unroll
+            for (int r = 0; r < RK; ++r) {
+                const int k = t + TPL * r;
+                if ((M + 1) % TPL != 0 && r == RK - 1 && k > M) break;
+                emit(l, k);
+            }
+        }
+    } else {
+        using RO = FftRounds<LPB * (M + 1), NTH>;
+#pragma unroll
+        for (int j0 = 0; j0 < RO::R; ++j0) {
+            const int idx = tid + NTH * j0;
+            if (!RO::ok(idx)) continue;
+            int l, k;
+            if (CONTIG) { l = idx / (M + 1); k = idx - l * (M + 1); }
+            else { k = idx / LPB; l = idx - k * LPB; }
+            if (l >= f.nl) continue;
+            emit(l, k);
+        }
     }
 }
 
@@ -1083,6 +1163,7 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
     constexpr int M = G::M, N = G::N, LPB = G::LPB, LS = G::LS;
     __shared__ double L[LPB * LS];
     __shared__ double CS[fft_cs_len<M2>()];   // prime stage-2 roots (LdsPrime rows only)
+    __shared__ __attribute__((aligned(16))) double PT[G::PT_LDS ? G::PTN : 2];
 #if FOTO_FFT_TW_LDS
     __shared__ double TW[2 * M];
 #else
@@ -1092,6 +1173,7 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
     const FftLines f = fft_lines<CONTIG, LPB>(outer, inner);
     if constexpr (LdsPrime<M2>::value)
         for (int p = tid; p < 2 * M2; p += NTH) CS[p] = tab[6 * M + 6 + p];
+    fft_pt_fill<G>(PT, tab);
     const int64_t st = CONTIG ? 1 : inner;
     auto base = [&](int l) -> int64_t {
         return CONTIG ? (int64_t)(f.o0 + l) * N : (int64_t)f.o0 * N * inner + f.i0 + l;
@@ -1108,15 +1190,28 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
     // image of X, so Z is written once and nothing is held in registers across a barrier)
     constexpr int MH = M / 2 + 1;
     using RP = FftRounds<LPB * MH, NTH>;
+    // element j0 of this thread: (line l, k); contiguous lines by line thread groups (round 6)
+    constexpr bool LT = CONTIG && FOTO_FFT_LINE_THREADS && NTH % LPB == 0 &&
+                        (MH + NTH / LPB - 1) / (NTH / LPB) == RP::R;
+    auto lk = [&](int j0, int& l, int& k) -> bool {
+        if constexpr (LT) {
+            l = tid / (NTH / LPB);
+            k = tid - l * (NTH / LPB) + (NTH / LPB) * j0;
+            return k < MH;
+        } else {
+            const int idx = tid + NTH * j0;
+            if (CONTIG) { l = idx / MH; k = idx - l * MH; }
+            else { k = idx / LPB; l = idx - k * LPB; }
+            return RP::ok(idx);
+        }
+    };
     double xk[RP::R], xnk[RP::R], xmk[RP::R], xpk[RP::R];   // X_k, X_{N-k}, X_{M-k}, X_{N-M+k}
 #pragma unroll
     for (int j0 = 0; j0 < RP::R; ++j0) {   // all rounds' loads first
-        const int idx = tid + NTH * j0;
         int l, k;
-        if (CONTIG) { l = idx / MH; k = idx - l * MH; }
-        else { k = idx / LPB; l = idx - k * LPB; }
+        const bool ok = lk(j0, l, k);
         xk[j0] = xnk[j0] = xmk[j0] = xpk[j0] = 0.0;
-        if (RP::ok(idx) && l < f.nl) {
+        if (ok && l < f.nl) {
             const double* X = in + base(l);
             xk[j0] = ld_dead(&X[k * st]);
             if (k != 0) xnk[j0] = ld_dead(&X[(N - k) * st]);
@@ -1124,17 +1219,23 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
             if (M - k != 0) xpk[j0] = ld_dead(&X[(N - (M - k)) * st]);
         }
     }
+    if constexpr (G::PT_LDS) __syncthreads();   // (PT; the X loads stay in flight across it)
 #pragma unroll
     for (int j0 = 0; j0 < RP::R; ++j0) {
-        const int idx = tid + NTH * j0;
-        if (!RP::ok(idx)) continue;
         int l, k;
-        if (CONTIG) { l = idx / MH; k = idx - l * MH; }
-        else { k = idx / LPB; l = idx - k * LPB; }
+        if (!lk(j0, l, k)) continue;
         // V_j = e^{+i pi j/(2N)} Y_j, Y_j = (X_j / s_j, -X_{N-j} / s_{N-j}), j in {k, M - k}
         auto V = [&](int j, double xj, double xnj, double& vr, double& vi) {
             const double yr = xj * (j == 0 ? is0 : is), yi = (j == 0) ? 0.0 : -xnj * is;
-            const double wbr = PB[2 * j], wbi = -PB[2 * j + 1];
+            double wbr, wbi;
+            if constexpr (G::PT_LDS) {
+                const dbl2 b = *reinterpret_cast<const dbl2*>(&PT[4 * j + 2]);
+                wbr = b.x;
+                wbi = -b.y;
+            } else {
+                wbr = PB[2 * j];
+                wbi = -PB[2 * j + 1];
+            }
             vr = fma(wbr, yr, -wbi * yi);
             vi = fma(wbr, yi, wbi * yr);
         };
@@ -1143,7 +1244,15 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
             bi = -bi;                                                  // conj V_{M-q} = V_{q+M}
             const double er = 0.5 * (ar + br), ei = 0.5 * (ai + bi);   // Ve_q
             const double dr = 0.5 * (ar - br), di = 0.5 * (ai - bi);
-            const double war = PA[2 * q], wai = -PA[2 * q + 1];        // e^{+2 pi i q/N}
+            double war, wai;                                           // e^{+2 pi i q/N}
+            if constexpr (G::PT_LDS) {
+                const dbl2 a = *reinterpret_cast<const dbl2*>(&PT[4 * q]);
+                war = a.x;
+                wai = -a.y;
+            } else {
+                war = PA[2 * q];
+                wai = -PA[2 * q + 1];
+            }
             const double orr = fma(war, dr, -wai * di), oi = fma(war, di, wai * dr);   // Vo_q
             zr = er - oi;                                              // Z = Ve + i Vo
             zi = ei + orr;
@@ -1164,22 +1273,37 @@ __global__ __launch_bounds__(NTH) void k_dct_fft_inv(int outer, int inner, const
         }
     }
     __syncthreads();
-    fft_stage1<M1, M2, true, LPB, NTH>(L, TW);
+    fft_stage1<M1, M2, true, LPB, NTH, G::PT_LDS && FOTO_FFT_TW_PT>(L, TW, PT);
     __syncthreads();
     fft_stage2_any<M1, M2, true, LPB, NTH>(L, CS);
     __syncthreads();
     constexpr double iM = 1.0 / M;
-    using RS = FftRounds<LPB * N, NTH>;
+    if constexpr (CONTIG && FOTO_FFT_LINE_THREADS && NTH % LPB == 0 && N % (NTH / LPB) == 0) {
+        constexpr int TPL = NTH / LPB, RI = N / TPL;   // (round 6) a fixed line per thread group
+        const int l = tid / TPL, t = tid - l * TPL;
+        if (l < f.nl) {
+            const double* Ll = L + l * LS;
+            double* o = out + base(l);
 #pragma unroll
-    for (int j0 = 0; j0 < RS::R; ++j0) {   // x_i = v_p, p = Makhoul position of i
-        const int idx = tid + NTH * j0;
-        if (!RS::ok(idx)) continue;
-        int l, i;
-        if (CONTIG) { l = idx / N; i = idx - l * N; }
-        else { i = idx / LPB; l = idx - i * LPB; }
-        if (l >= f.nl) continue;
-        const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
-        out[base(l) + i * st] = L[l * LS + 2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
+            for (int r = 0; r < RI; ++r) {   // x_i = v_p, p = Makhoul position of i
+                const int i = t + TPL * r;
+                const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
+                o[i] = Ll[2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
+            }
+        }
+    } else {
+        using RS = FftRounds<LPB * N, NTH>;
+#pragma unroll
+        for (int j0 = 0; j0 < RS::R; ++j0) {   // x_i = v_p, p = Makhoul position of i
+            const int idx = tid + NTH * j0;
+            if (!RS::ok(idx)) continue;
+            int l, i;
+            if (CONTIG) { l = idx / N; i = idx - l * N; }
+            else { i = idx / LPB; l = idx - i * LPB; }
+            if (l >= f.nl) continue;
+            const int p = (i & 1) ? N - 1 - (i >> 1) : (i >> 1);
+            out[base(l) + i * st] = L[l * LS + 2 * fft_pos<M1, M2>(p >> 1) + (p & 1)] * iM;
+        }
     }
 }
 
