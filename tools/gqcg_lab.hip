@@ -473,6 +473,23 @@ __global__ __launch_bounds__(256) void k_cg_r6(const GqNodes* __restrict__ nd, d
             const dbl4 d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(u, 1.0, dbl4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
             *wa = d2[0];
             *wb = d2[2];
+        } else if constexpr (RED == 3) {
+            // reduce-scatter by one permlane32 swap pair (a-partials in lanes 0-31, b-partials in
+            // 32-63), xor 16 by permlane16 swaps, then an all-reduce inside each 16-lane row by
+            // DPP rotations (8, 4, 2, 1): every lane of the low half ends with the a total, of the
+            // high half with the b total -- one double per level after the first
+            const long long ba = __double_as_longlong(a), bb = __double_as_longlong(b);
+            auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ba, (unsigned)bb, false, false);
+            auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ba >> 32), (unsigned)(bb >> 32), false, false);
+            double t = __longlong_as_double(((long long)hi[0] << 32) | lo[0]) +
+                       __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+            t += dbl_pl16(t);
+            t += dbl_dpp<0x128>(t);   // row_ror:8
+            t += dbl_dpp<0x124>(t);   // row_ror:4
+            t += dbl_dpp<0x122>(t);   // row_ror:2
+            t += dbl_dpp<0x121>(t);   // row_ror:1
+            *wa = dbl_readlane(t, 0);
+            *wb = dbl_readlane(t, 32);
         } else {
             *wa = 64.0 * a;
             *wb = 64.0 * b;
@@ -623,6 +640,8 @@ int main(int argc, char** argv) {
         timeit("r6 dpp+lds fast 1/rho", [&] { k_cg_r6<0, 0, 1><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
         timeit("r6 mfma+lds", [&] { k_cg_r6<1, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
         timeit("r6 mfma+lds fast 1/rho", [&] { k_cg_r6<1, 0, 1><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 rotate+lds", [&] { k_cg_r6<3, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, true);
+        timeit("r6 rotate only (no lds)", [&] { k_cg_r6<3, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
         timeit("r6 dpp only (no lds)", [&] { k_cg_r6<0, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
         timeit("r6 mfma only (no lds)", [&] { k_cg_r6<1, 1, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
         timeit("r6 lds only (no wave red)", [&] { k_cg_r6<2, 0, 0><<<1, 256>>>(nd, 0.0, maxiter, S1); }, false);
