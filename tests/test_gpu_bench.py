@@ -106,6 +106,16 @@ def test_bench_n8_line_time_sharded_headline():
     assert d["c4"] is None
 
 
+def test_bench_n4_line_with_c4():
+    """N = 4, as the driver's scaling run launches it: eight planes per rank on the metric grid,
+    and config 4 sharded over the same four ranks (16 planes each) in "c4"."""
+    d = _ranks(4, 29620, args=("--c4-steps", "1", "--c4-warmup", "1"))
+    _check_strong(d, 4)
+    assert d["sharded"]["planes_per_rank"] == [8] * 4
+    c4 = d["c4"]
+    assert c4["value"] > 0 and c4["rccl_ranks"] == 4 and c4["planes_per_rank"] == [16] * 4, c4
+
+
 def test_bench_rccl_failure_gives_null_value():
     """An RCCL failure (the mock refuses the communicator, as real RCCL refuses two ranks on one
     GPU): the headline value is null with the error in the line -- the batch number, which

@@ -85,7 +85,7 @@ def compare(ranks, virt, Nt, Nx, Ny, W):
 
 
 @pytest.mark.parametrize("cg_mode", [2, 3])
-@pytest.mark.parametrize("W", [2, 3, 5, 8])
+@pytest.mark.parametrize("W", [2, 3, 4, 5, 8])
 def test_rccl_path_bit_identical_to_virtual_ranks(W, cg_mode):
     """cg_mode 2: one moment all-gather per s-step pass; cg_mode 3: one histogram all-gather
     (4096 doubles) per CG solve."""
@@ -156,6 +156,20 @@ def test_rccl_path_c4_w8():
     one = run_virtual(L, 1, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
     assert all(abs(a - b) <= 1 for a, b in zip(ranks[0]["cg"], one["cg"]))
     np.testing.assert_allclose(ranks[0]["crit"], one["crit"], rtol=1e-7)
+    assert all(r["redo"] == 0 for r in ranks)
+
+
+def test_rccl_path_c4_w4():
+    """The driver's N = 4 scaling run of config 4: 16 planes and 256 rows per rank, the default
+    pipelined all-to-alls with the phi halo inside the backward one (planes of 2^20 voxels) --
+    bit-identical to the same decomposition as virtual ranks."""
+    from foto.synthetic import translating_gaussian
+    Nt, Nx, Ny, W = 64, 1024, 1024, 4
+    rho0, rhoT = translating_gaussian(Nx, Ny)
+    L = _mock()
+    ranks = run_ranks(L, W, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
+    virt = run_virtual(L, W, rho0, rhoT, Nt, Nx, Ny, iters=2, cg_mode=3)
+    compare(ranks, virt, Nt, Nx, Ny, W)
     assert all(r["redo"] == 0 for r in ranks)
 
 
