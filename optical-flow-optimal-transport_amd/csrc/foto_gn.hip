@@ -14,9 +14,13 @@
 #include "foto_internal.h"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace foto {
@@ -707,6 +711,7 @@ __global__ __launch_bounds__(NT) void k_mg_b0(int64_t n, const double* __restric
 }
 
 // coarse B = (sum of children B weighted by the P weights) / (sum of those weights)
+// (FOTO_GN_SETUP_FUSE=0: this form and k_mg_dinv; default: k_mg_coarsen_d)
 __global__ __launch_bounds__(NT) void k_mg_coarsen(int w, int h, const double* __restrict__ B, int wc, int hc,
                                                    double* __restrict__ Bc) {
     const int64_t nc = (int64_t)wc * hc, n = (int64_t)w * h;
@@ -729,16 +734,13 @@ __global__ __launch_bounds__(NT) void k_mg_coarsen(int w, int h, const double* _
     for (int f = 0; f < 6; ++f) Bc[f * nc + I] = acc[f] / ws;
 }
 
-// inverse of the 3x3 diagonal block diag(s c) + B (symmetric positive definite), cofactors
-__global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Dinv) {
+// inverse of the 3x3 diagonal block diag(s c) + B (symmetric positive definite), cofactors, of
+// cell (x, y) = i of level L from its B values
+__device__ __forceinline__ void mg_dinv_cell(const MGLev& L, int x, int y, int64_t i, const double* Bv,
+                                             double* __restrict__ Dinv) {
     const int64_t n = (int64_t)L.w * L.h;
-    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-    if (i >= n) return;
-    const int y = (int)(i / L.w), x = (int)(i - (int64_t)y * L.w);
     const double c = (double)mg_ncount(x, y, L.w, L.h);
-    const double* B = L.B;
-    const double a = L.s0 * c + B[i], b = B[n + i], d = B[2 * n + i], e = L.s1 * c + B[3 * n + i],
-                 f = B[4 * n + i], g = L.s2 * c + B[5 * n + i];
+    const double a = L.s0 * c + Bv[0], b = Bv[1], d = Bv[2], e = L.s1 * c + Bv[3], f = Bv[4], g = L.s2 * c + Bv[5];
     // [[a b d] [b e f] [d f g]]
     const double c00 = e * g - f * f, c01 = d * f - b * g, c02 = b * f - d * e;
     const double c11 = a * g - d * d, c12 = b * d - a * f, c22 = a * e - b * b;
@@ -749,6 +751,75 @@ __global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Di
     Dinv[3 * n + i] = c11 * id;
     Dinv[4 * n + i] = c12 * id;
     Dinv[5 * n + i] = c22 * id;
+}
+
+__global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Dinv) {
+    const int64_t n = (int64_t)L.w * L.h;
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const int y = (int)(i / L.w), x = (int)(i - (int64_t)y * L.w);
+    const double Bv[6] = {L.B[i], L.B[n + i], L.B[2 * n + i], L.B[3 * n + i], L.B[4 * n + i], L.B[5 * n + i]};
+    mg_dinv_cell(L, x, y, i, Bv, Dinv);
+}
+
+// Round 6 (setup of a solve, 0.3 ms at 640x480 of which the coarsening was ~95 us over five
+// launches and the block inverses six more): level 0's B with its block inverses in one pass, and
+// each coarse level's B with its block inverses in one pass over a fixed 4 x 4 window (clamped
+// addresses, every load issued at once; positions of weight 0 are skipped as before, so the sums
+// are the same in the same order: bit-identical to k_mg_b0 / k_mg_coarsen + k_mg_dinv)
+__global__ __launch_bounds__(NT) void k_mg_b0_d(MGLev L, const double* __restrict__ fx, const double* __restrict__ fy,
+                                                const double* __restrict__ f2, double* __restrict__ B,
+                                                double* __restrict__ Dinv) {
+    const int n = L.w * L.h;
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const double a = fx[i], b = fy[i], m = f2[i];
+    const double Bv[6] = {a * a, a * b, -a * m, b * b, -b * m, m * m};
+#pragma unroll
+    for (int f = 0; f < 6; ++f) B[(int64_t)f * n + i] = Bv[f];
+    const int y = i / L.w;
+    mg_dinv_cell(L, i - y * L.w, y, i, Bv, Dinv);
+}
+
+__global__ __launch_bounds__(NT) void k_mg_coarsen_d(int w, int h, const double* __restrict__ B, MGLev C,
+                                                     double* __restrict__ Bc, double* __restrict__ Dinv) {
+    const int nc = C.w * C.h, n = w * h;
+    const int I = blockIdx.x * NT + threadIdx.x;
+    if (I >= nc) return;
+    const int J = I / C.w, K = I - J * C.w;
+    double wy[4], wx[4];
+    int ro[4], co[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int y = 2 * J - 1 + t, x = 2 * K - 1 + t;
+        wy[t] = (y >= 0 && y < h) ? mg_w1(y, J, C.h) : 0.0;
+        wx[t] = (x >= 0 && x < w) ? mg_w1(x, K, C.w) : 0.0;
+        ro[t] = min(max(y, 0), h - 1) * w;
+        co[t] = min(max(x, 0), w - 1);
+    }
+    double acc[6] = {0, 0, 0, 0, 0, 0}, ws = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double wgt = wy[t] * wx[u];
+            const int i = ro[t] + co[u];
+            double v[6];
+#pragma unroll
+            for (int f = 0; f < 6; ++f) v[f] = B[(int64_t)f * n + i];
+            if (wgt != 0.0) {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) acc[f] += wgt * v[f];
+                ws += wgt;
+            }
+        }
+    double Bv[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+        Bv[f] = acc[f] / ws;
+        Bc[(int64_t)f * nc + I] = Bv[f];
+    }
+    mg_dinv_cell(C, K, J, I, Bv, Dinv);
 }
 
 // k_gnp_upd folded into the level-0 down leg (round 5; FOTO_GN_FOLD=0: the separate kernel):
@@ -1717,6 +1788,95 @@ __global__ __launch_bounds__(MG_LT_NTH) void k_mg_ltail(MGLev L, MGLev C, const 
 
 using namespace foto;
 
+namespace {
+
+// The host side of a solve is two copies between the caller's pageable arrays and the plan's
+// pinned staging: 5 MB in, 7.4 MB out at 640x480, 0.13 + 0.22 ms on one core against a 4.6 ms
+// solve (FOTO_GN_TRACE).  A few workers made with the staging split them; the caller takes a
+// share too.  FOTO_GN_HOST_THREADS (default 4) counts the workers; 0 copies on the caller alone.
+class HostPool {
+public:
+    explicit HostPool(int workers) {
+        for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int workers() const { return (int)th_.size(); }
+    // f(i) for every i < n, on the workers and the caller; returns when all have run
+    void run(int n, const std::function<void(int)>& f) {
+        if (th_.empty() || n <= 1) {
+            for (int i = 0; i < n; ++i) f(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &f;
+            n_ = n;
+            next_.store(0);
+            pending_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void drain() {
+        for (int i; (i = next_.fetch_add(1)) < n_;) (*job_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            drain();
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                --pending_;
+            }
+            done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, pending_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// memcpy in pieces of at least 256 KB over the pool
+void pool_memcpy(HostPool* pool, void* dst, const void* src, size_t bytes) {
+    const size_t piece = 256 << 10;
+    const int parts = pool ? (int)std::min<size_t>((size_t)pool->workers() + 1, (bytes + piece - 1) / piece) : 1;
+    if (parts <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t step = ((bytes + parts - 1) / parts + 4095) & ~(size_t)4095;
+    pool->run(parts, [&](int i) {
+        const size_t a = (size_t)i * step;
+        if (a < bytes) memcpy((char*)dst + a, (const char*)src + a, std::min(step, bytes - a));
+    });
+}
+
+}  // namespace
+
 struct foto_gn_plan {
     int w = 0, h = 0, maxiter = 0, device = 0;
     double alpha = 0, lam = 0, rtol = 0;
@@ -1726,6 +1886,8 @@ struct foto_gn_plan {
            *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr;
     double *rr_part = nullptr, *pq_part = nullptr, *rz_part[2] = {nullptr, nullptr};
     double *r2 = nullptr, *q = nullptr, *rr_part2 = nullptr;   // the folded update (fold)
+    bool exact_tail = true;          // launch the predicted count exactly (FOTO_GN_EXACT=0: whole graphs)
+    bool setup_fuse = true;          // B and block inverses per level in one pass (FOTO_GN_SETUP_FUSE=0: not)
     bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
     size_t pt_l0 = 0;                // first level of the persistent small-level launch (0: none; FOTO_MG_PTAIL=1: on)
     bool lt = false;                 // the last level + coarsest in one LDS-resident block (k_mg_ltail)
@@ -1746,6 +1908,8 @@ struct foto_gn_plan {
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t dl_ev[3] = {nullptr, nullptr, nullptr};   // u, v, m downloaded (the copy-out of one overlaps the next)
+    std::unique_ptr<HostPool> pool;                        // host copies (made with the staging)
     int last_its = 0;
     double last[4] = {0, 0, 0, 0};   // ms setup+upload, ms PCG, iterations, iterations launched
     bool tail = false;               // small levels in one block (k_mg_tail, FOTO_MG_TAIL=1; measured slower)
@@ -1759,6 +1923,8 @@ struct foto_gn_plan {
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (graph) (void)hipGraphDestroy(graph);
         for (auto e : ev) if (e) (void)hipEventDestroy(e);
+        for (auto e : dl_ev) if (e) (void)hipEventDestroy(e);
+        pool.reset();
         if (base) (void)hipFree(base);
         if (hS) (void)hipHostFree(hS);
         if (hbuf) (void)hipHostFree(hbuf);
@@ -1931,6 +2097,7 @@ static int gn_plan_init(foto_gn_plan* P) {
     FOTO_TRY(stream_acquire(&P->s));   // (pooled: a new stream cost ~10 ms)
     tr.mark("stream");
     for (auto& e : P->ev) FOTO_HIP_CHECK(hipEventCreate(&e));
+    for (auto& e : P->dl_ev) FOTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     tr.mark("events");
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hS, sizeof(CGScal)));
     tr.mark("pinned scalars");   // (the pinned staging is made during the first solve: gn_staging)
@@ -1956,6 +2123,10 @@ static int gn_plan_init(foto_gn_plan* P) {
     }
     P->nb_rz = P->lev.size() == 1 ? 1 : mg_tiles(w, h);
     {
+        const char* sf = getenv("FOTO_GN_SETUP_FUSE");
+        P->setup_fuse = !(sf && atoi(sf) == 0);
+        const char* ex = getenv("FOTO_GN_EXACT");
+        P->exact_tail = !(ex && atoi(ex) == 0);
         const char* e = getenv("FOTO_GN_FOLD");
         P->fold = P->lev.size() > 1 && !(e && atoi(e) == 0);   // (one level: no down leg to fold into)
     }
@@ -2037,6 +2208,9 @@ static int gn_staging(foto_gn_plan* P) {
     FOTO_HIP_CHECK(hipHostMalloc((void**)&P->hbuf, 5 * n * sizeof(double)));
     memset(P->hbuf, 0, 5 * n * sizeof(double));   // first touch on the host, not by the device
     FOTO_HIP_CHECK(hipHostGetDevicePointer((void**)&P->hbuf_dev, P->hbuf, 0));
+    const char* e = getenv("FOTO_GN_HOST_THREADS");
+    const int workers = e ? std::max(0, std::min(16, atoi(e))) : 4;
+    if (workers > 0) P->pool = std::make_unique<HostPool>(workers);
     return 0;
 }
 
@@ -2049,31 +2223,43 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     FOTO_HIP_CHECK(hipEventRecord(P->ev[0], s));
     if (P->hbuf) {
         double* hb = P->hbuf;
-        memcpy(hb, f1, n * sizeof(double));
+        pool_memcpy(P->pool.get(), hb, f1, n * sizeof(double));
         FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, hb, n * sizeof(double), hipMemcpyHostToDevice, s));
-        memcpy(hb + n, f2, n * sizeof(double));
+        pool_memcpy(P->pool.get(), hb + n, f2, n * sizeof(double));
         FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, hb + n, n * sizeof(double), hipMemcpyHostToDevice, s));
     } else {   // first solve of the plan (gn_staging)
         FOTO_HIP_CHECK(hipMemcpyAsync(P->d1, f1, n * sizeof(double), hipMemcpyHostToDevice, s));
         FOTO_HIP_CHECK(hipMemcpyAsync(P->d2, f2, n * sizeof(double), hipMemcpyHostToDevice, s));
     }
+    tr.mark("solve: upload staged");
     FOTO_HIP_CHECK(hipMemsetAsync(P->dS, 0, sizeof(CGScal), s));
     if (P->pt_l0 > 0) FOTO_HIP_CHECK(hipMemsetAsync(P->pt_counter, 0, sizeof(unsigned), s));
     FOTO_HIP_CHECK(hipMemsetAsync(P->x, 0, 3 * n * sizeof(double), s));
     FOTO_HIP_CHECK(launch_gn_coeffs(w, h, P->d1, P->d2, P->fx, P->fy, P->ft, s));
     FOTO_HIP_CHECK(launch_gn_rhs(w, h, P->fx, P->fy, P->d2, P->ft, P->b, s));
     // image-dependent multigrid coefficients
-    k_mg_b0<<<flat_blocks(n), NT, 0, s>>>(n, P->fx, P->fy, P->d2, P->lev[0].B);
-    FOTO_HIP_CHECK(hipGetLastError());
-    for (size_t l = 1; l < P->lev.size(); ++l) {
-        const auto& L = P->lev[l - 1];
-        const auto& C = P->lev[l];
-        k_mg_coarsen<<<flat_blocks((int64_t)C.w * C.h), NT, 0, s>>>(L.w, L.h, L.B, C.w, C.h, C.B);
+    if (P->setup_fuse) {
+        k_mg_b0_d<<<flat_blocks(n), NT, 0, s>>>(P->desc(0), P->fx, P->fy, P->d2, P->lev[0].B, P->lev[0].Dinv);
         FOTO_HIP_CHECK(hipGetLastError());
-    }
-    for (size_t l = 0; l < P->lev.size(); ++l) {
-        k_mg_dinv<<<flat_blocks((int64_t)P->lev[l].w * P->lev[l].h), NT, 0, s>>>(P->desc(l), P->lev[l].Dinv);
+        for (size_t l = 1; l < P->lev.size(); ++l) {
+            const auto& L = P->lev[l - 1];
+            const auto& C = P->lev[l];
+            k_mg_coarsen_d<<<flat_blocks((int64_t)C.w * C.h), NT, 0, s>>>(L.w, L.h, L.B, P->desc(l), C.B, C.Dinv);
+            FOTO_HIP_CHECK(hipGetLastError());
+        }
+    } else {
+        k_mg_b0<<<flat_blocks(n), NT, 0, s>>>(n, P->fx, P->fy, P->d2, P->lev[0].B);
         FOTO_HIP_CHECK(hipGetLastError());
+        for (size_t l = 1; l < P->lev.size(); ++l) {
+            const auto& L = P->lev[l - 1];
+            const auto& C = P->lev[l];
+            k_mg_coarsen<<<flat_blocks((int64_t)C.w * C.h), NT, 0, s>>>(L.w, L.h, L.B, C.w, C.h, C.B);
+            FOTO_HIP_CHECK(hipGetLastError());
+        }
+        for (size_t l = 0; l < P->lev.size(); ++l) {
+            k_mg_dinv<<<flat_blocks((int64_t)P->lev[l].w * P->lev[l].h), NT, 0, s>>>(P->desc(l), P->lev[l].Dinv);
+            FOTO_HIP_CHECK(hipGetLastError());
+        }
     }
     // r = b, r.r; z_0 = V(r), r.z -> rz_part[0]
     k_gnp_init<<<P->nb_pix, NT, 0, s>>>(n, P->b, P->r, P->rr_part);
@@ -2089,11 +2275,19 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     const int maxiter = P->maxiter;
     const int G = P->graph_its;
     const int first = P->last_its > 0 ? ((P->last_its + 1 + G - 1) / G) * G : 16;
+    // (round 6: a reused plan launches exactly its predicted its + 1, the remainder past whole
+    // graphs as single iterations -- a graph's surplus iterations each cost ~25 us of early exits)
+    const int first_exact = P->last_its > 0 ? P->last_its + 1 : 16;
     while (k < maxiter) {
-        const int chunk = std::min(k == 0 ? first : G, maxiter - k);
+        const int chunk = std::min(k == 0 ? (P->exact_tail ? first_exact : first) : G, maxiter - k);
         int j = 0;
+        if ((k & 1) && chunk > 0) {   // (after an under-predicted exact count: the graph starts on parity 0)
+            FOTO_TRY(gn_iteration(P, 1));
+            ++j;
+            ++k;
+        }
         for (; j + G <= chunk; j += G, k += G) FOTO_HIP_CHECK(hipGraphLaunch(P->gexec, s));
-        for (; j < chunk; ++j, ++k) FOTO_TRY(gn_iteration(P, k & 1));   // (maxiter's remainder, outside the graph)
+        for (; j < chunk; ++j, ++k) FOTO_TRY(gn_iteration(P, k & 1));   // (the remainder, outside the graph)
         FOTO_HIP_CHECK(hipMemcpyAsync(P->hS, P->dS, sizeof(CGScal), hipMemcpyDeviceToHost, s));
         if (k == chunk) FOTO_TRY(gn_staging(P));   // while the first iterations run
         FOTO_HIP_CHECK(hipStreamSynchronize(s));
@@ -2108,14 +2302,19 @@ static int gn_plan_solve(foto_gn_plan* P, const double* f1, const double* f2, do
     // the solution straight into the mapped pinned staging by a kernel: the first large
     // device-to-host hipMemcpy of a process took 8.5-14.8 ms at 640x480 (0.15-0.4 ms later)
     FOTO_TRY(gn_staging(P));   // (maxiter 0: no iteration ran)
-    k_gn_download<<<flat_blocks(3 * n), NT, 0, s>>>(3 * n, P->x, P->hbuf_dev + 2 * n);
-    FOTO_HIP_CHECK(hipGetLastError());
-    FOTO_HIP_CHECK(hipStreamSynchronize(s));
-    tr.mark("solve: download");
-    const double* hb = P->hbuf;
-    memcpy(u, hb + 2 * n, n * sizeof(double));
-    memcpy(v, hb + 3 * n, n * sizeof(double));
-    memcpy(m, hb + 4 * n, n * sizeof(double));
+    // u, v, m one after the other, each copied out while the next crosses PCIe
+    double* const outs[3] = {u, v, m};
+    for (int c = 0; c < 3; ++c) {
+        k_gn_download<<<flat_blocks(n), NT, 0, s>>>(n, P->x + c * n, P->hbuf_dev + (2 + c) * n);
+        FOTO_HIP_CHECK(hipGetLastError());
+        FOTO_HIP_CHECK(hipEventRecord(P->dl_ev[c], s));
+    }
+    for (int c = 0; c < 3; ++c) {
+        FOTO_HIP_CHECK(hipEventSynchronize(P->dl_ev[c]));
+        if (c == 0) tr.mark("solve: download u");
+        pool_memcpy(P->pool.get(), outs[c], P->hbuf + (2 + c) * n, n * sizeof(double));
+    }
+    tr.mark("solve: copy out");
     const int its = done ? P->hS->iters : maxiter;
     float t0 = 0.f, t1 = 0.f;
     FOTO_HIP_CHECK(hipEventElapsedTime(&t0, P->ev[0], P->ev[1]));
