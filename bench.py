@@ -213,11 +213,12 @@ def gn_levels(w, h, coarse=1024):
 def gn_bytes_per_iteration(w, h):
     """Algorithmic HBM bytes of one MG-PCG iteration: k_gnp_dir 12 n, k_gnp_upd
     18 n, per level k_mg_down2 18 n_l + 3 n_l+1 and k_mg_up2 21 n_l + 3 n_l+1, the coarsest
-    level 18 n_c fp64 values."""
+    level 18 n_c fp64 values -- except level 0, whose legs form B and D^-1 from (fx, fy, f2)
+    instead of loading them (round 6): down 9 n_0, up 12 n_0."""
     ns = gn_levels(w, h)
     v = 12 * ns[0] + 18 * ns[0]
     for l in range(len(ns) - 1):
-        v += 18 * ns[l] + 21 * ns[l] + 6 * ns[l + 1]
+        v += (9 + 12 if l == 0 else 18 + 21) * ns[l] + 6 * ns[l + 1]
     v += 18 * ns[-1]
     return 8 * v
 
@@ -262,7 +263,7 @@ def gn_side():
                     "us_per_pcg_it": round(1e3 * tm["ms_pcg"] / max(tm["iterations"], 1), 1),
                     "roofline": {"bound": "hbm", "alg_bytes_per_it": by, "achieved": round(ach, 1),
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                 "note": "PCG phase: 10 launches per iteration (the update folded into the level-0 down leg, the last level + coarsest in one LDS-resident block), 4 iterations per graph replay, small levels at the launch floor"}})
+                                 "note": "PCG phase: 10 launches per iteration (the update folded into the level-0 down leg, level 0's B and D^-1 formed from fx, fy, f2, the last level + coarsest in one LDS-resident block), 4 iterations per graph replay, small levels at the launch floor"}})
         out[f"gpu_{w}x{h}"] = rec
     return out
 

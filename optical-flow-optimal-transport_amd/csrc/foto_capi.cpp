@@ -284,8 +284,10 @@ int foto_gn_solve(const double* f1, const double* f2, int w, int h, double alpha
 }
 
 // Algorithmic HBM bytes of one MG-PCG iteration (bench.py gn_bytes_per_iteration):
-// k_gnp_dir 12 n, k_gnp_upd 18 n, per level k_mg_down2 18 n_l + 3 n_l+1 and k_mg_up2 21 n_l + 3 n_l+1,
-// the coarsest level 18 n_c fp64 values; levels halve (rounding up) until <= 1024 cells.
+// k_gnp_dir 12 n, k_gnp_upd 18 n, per level k_mg_down2 18 n_l + 3 n_l+1 and k_mg_up2 21 n_l + 3 n_l+1
+// (level 0: 9 n_0 and 12 n_0, its B and D^-1 formed from fx, fy, f2; FOTO_GN_RECOMP=0 loads them
+// and moves more than this counts), the coarsest level 18 n_c fp64 values; levels halve (rounding
+// up) until <= 1024 cells.
 static double gn_alg_bytes(int w, int h, int* levels) {
     std::vector<double> ns{(double)w * h};
     while ((double)w * h > 1024) {
@@ -294,7 +296,7 @@ static double gn_alg_bytes(int w, int h, int* levels) {
         ns.push_back((double)w * h);
     }
     double v = 30.0 * ns[0];
-    for (size_t l = 0; l + 1 < ns.size(); ++l) v += 39.0 * ns[l] + 6.0 * ns[l + 1];
+    for (size_t l = 0; l + 1 < ns.size(); ++l) v += (l == 0 ? 21.0 : 39.0) * ns[l] + 6.0 * ns[l + 1];
     v += 18.0 * ns.back();
     if (levels) *levels = (int)ns.size();
     return 8.0 * v;

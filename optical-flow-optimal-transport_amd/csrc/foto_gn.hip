@@ -735,23 +735,48 @@ __global__ __launch_bounds__(NT) void k_mg_coarsen(int w, int h, const double* _
 }
 
 // inverse of the 3x3 diagonal block diag(s c) + B (symmetric positive definite), cofactors, of
-// cell (x, y) = i of level L from its B values
-__device__ __forceinline__ void mg_dinv_cell(const MGLev& L, int x, int y, int64_t i, const double* Bv,
-                                             double* __restrict__ Dinv) {
-    const int64_t n = (int64_t)L.w * L.h;
+// cell (x, y) of level L from its B values
+__device__ __forceinline__ void mg_dinv_vals(const MGLev& L, int x, int y, const double* Bv, double (&D)[6]) {
     const double c = (double)mg_ncount(x, y, L.w, L.h);
     const double a = L.s0 * c + Bv[0], b = Bv[1], d = Bv[2], e = L.s1 * c + Bv[3], f = Bv[4], g = L.s2 * c + Bv[5];
     // [[a b d] [b e f] [d f g]]
     const double c00 = e * g - f * f, c01 = d * f - b * g, c02 = b * f - d * e;
     const double c11 = a * g - d * d, c12 = b * d - a * f, c22 = a * e - b * b;
     const double det = a * c00 + b * c01 + d * c02, id = 1.0 / det;
-    Dinv[i] = c00 * id;
-    Dinv[n + i] = c01 * id;
-    Dinv[2 * n + i] = c02 * id;
-    Dinv[3 * n + i] = c11 * id;
-    Dinv[4 * n + i] = c12 * id;
-    Dinv[5 * n + i] = c22 * id;
+    D[0] = c00 * id;
+    D[1] = c01 * id;
+    D[2] = c02 * id;
+    D[3] = c11 * id;
+    D[4] = c12 * id;
+    D[5] = c22 * id;
 }
+
+__device__ __forceinline__ void mg_dinv_cell(const MGLev& L, int x, int y, int64_t i, const double* Bv,
+                                             double* __restrict__ Dinv) {
+    const int64_t n = (int64_t)L.w * L.h;
+    double D[6];
+    mg_dinv_vals(L, x, y, Bv, D);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Dinv[k * n + i] = D[k];
+}
+
+// level 0's B of a cell from the GN coefficients (fx, fy, f2) there: v v^T, v = (fx, fy, -f2)
+__device__ __forceinline__ void mg_b_from(double a, double b, double m, double (&B)[6]) {
+    B[0] = a * a;
+    B[1] = a * b;
+    B[2] = -a * m;
+    B[3] = b * b;
+    B[4] = -b * m;
+    B[5] = m * m;
+}
+
+// the GN coefficient planes level 0's B and D^-1 are made of (round 6: the PCG's level-0 legs
+// form both per cell from these 24 B instead of loading the stored 96 B; FOTO_GN_RECOMP=0: load)
+struct MGCoef {
+    const double* fx;
+    const double* fy;
+    const double* f2;
+};
 
 __global__ __launch_bounds__(NT) void k_mg_dinv(MGLev L, double* __restrict__ Dinv) {
     const int64_t n = (int64_t)L.w * L.h;
@@ -773,8 +798,8 @@ __global__ __launch_bounds__(NT) void k_mg_b0_d(MGLev L, const double* __restric
     const int n = L.w * L.h;
     const int i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
-    const double a = fx[i], b = fy[i], m = f2[i];
-    const double Bv[6] = {a * a, a * b, -a * m, b * b, -b * m, m * m};
+    double Bv[6];
+    mg_b_from(fx[i], fy[i], f2[i], Bv);
 #pragma unroll
     for (int f = 0; f < 6; ++f) B[(int64_t)f * n + i] = Bv[f];
     const int y = i / L.w;
@@ -838,6 +863,7 @@ struct MGUpd {
     double* rr_part;
     CGScal* S;
     int nb_rz, nb_pq;
+    MGCoef cf;   // (RC: level 0's B and D^-1 from these)
 };
 
 // Down leg of one level, one GT_Y x GT_X fine tile per block:
@@ -851,7 +877,7 @@ struct MGUpd {
 #ifndef FOTO_MG_RSALIAS
 #define FOTO_MG_RSALIAS 1
 #endif
-template <bool UPD>
+template <bool UPD, bool RC = false>
 __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const CGScal* S,
                                                  const double* __restrict__ f, double* __restrict__ xg,
                                                  double* __restrict__ fc, MGUpd U) {
@@ -877,20 +903,31 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
     const int x0 = (blockIdx.x % tiles_x) * GT_X, y0 = (blockIdx.x / tiles_x) * GT_Y;
     // stage-2 cells' B (tile + 1 halo); level 0 of a PCG iteration (UPD, FOTO_MG_B2LATE=1): after
     // stage 1 -- held from the start beside the stage-1 loads it took 150 VGPRs (3 waves per SIMD)
-    double b2[C2][6];
+    static_assert(!RC || UPD, "RC: the level-0 leg of a PCG iteration");
+    constexpr int NB = RC ? 3 : 6;   // per stage-2 cell: (fx, fy, f2) or B
+    double b2[C2][NB];
     auto load_b2 = [&]() {
 #pragma unroll
         for (int k = 0; k < C2; ++k) {
             const int c = threadIdx.x + k * NT;
             const int ly = c / RW, lx = c - ly * RW, gy = y0 - 1 + ly, gx = x0 - 1 + lx;
-            if (c < RH * RW && gx >= 0 && gx < w && gy >= 0 && gy < h) mg_load6(L.B, n, (int64_t)gy * w + gx, b2[k]);
-            else { for (int q = 0; q < 6; ++q) b2[k][q] = 0.0; }
+            if (c < RH * RW && gx >= 0 && gx < w && gy >= 0 && gy < h) {
+                const int64_t i = (int64_t)gy * w + gx;
+                if constexpr (RC) {
+                    b2[k][0] = U.cf.fx[i]; b2[k][1] = U.cf.fy[i]; b2[k][2] = U.cf.f2[i];
+                } else {
+                    for (int q = 0; q < 6; ++q) b2[k][q] = L.B[q * n + i];
+                }
+            } else {
+                for (int q = 0; q < NB; ++q) b2[k][q] = 0.0;
+            }
         }
     };
     constexpr bool B2LATE = UPD && FOTO_MG_B2LATE;
     if constexpr (!B2LATE) load_b2();
-    // stage-1 cells' f (UPD: r and q) and D^-1 (tile + 2 halo)
-    double f1[C1][3], d1[C1][6];
+    // stage-1 cells' f (UPD: r and q) and D^-1 (tile + 2 halo; RC: the coefficients it is made of)
+    constexpr int ND = RC ? 3 : 6;
+    double f1[C1][3], d1[C1][ND];
 #pragma unroll
     for (int k = 0; k < C1; ++k) {
         const int c = threadIdx.x + k * NT;
@@ -902,10 +939,14 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
             } else {
                 f1[k][0] = f[i]; f1[k][1] = f[n + i]; f1[k][2] = f[2 * n + i];
             }
-            mg_load6(L.Dinv, n, i, d1[k]);
+            if constexpr (RC) {
+                d1[k][0] = U.cf.fx[i]; d1[k][1] = U.cf.fy[i]; d1[k][2] = U.cf.f2[i];
+            } else {
+                for (int q = 0; q < 6; ++q) d1[k][q] = L.Dinv[q * n + i];
+            }
         } else {
             f1[k][0] = f1[k][1] = f1[k][2] = 0.0;
-            for (int q = 0; q < 6; ++q) d1[k][q] = 0.0;
+            for (int q = 0; q < ND; ++q) d1[k][q] = 0.0;
         }
     }
     double alpha = 0.0;
@@ -941,7 +982,14 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
         const int ly = c / XW, lx = c - ly * XW, gy = y0 - 2 + ly, gx = x0 - 2 + lx;
         double z0 = 0.0, z1 = 0.0, z2 = 0.0;
         if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
-            mg_dinv_v(d1[k], f1[k][0], f1[k][1], f1[k][2], z0, z1, z2);
+            if constexpr (RC) {
+                double Bv[6], D[6];
+                mg_b_from(d1[k][0], d1[k][1], d1[k][2], Bv);
+                mg_dinv_vals(L, gx, gy, Bv, D);
+                mg_dinv_v(D, f1[k][0], f1[k][1], f1[k][2], z0, z1, z2);
+            } else {
+                mg_dinv_v(d1[k], f1[k][0], f1[k][1], f1[k][2], z0, z1, z2);
+            }
             z0 *= MG_OMEGA; z1 *= MG_OMEGA; z2 *= MG_OMEGA;
         }
         xs[0][ly][lx] = z0; xs[1][ly][lx] = z1; xs[2][ly][lx] = z2;
@@ -961,7 +1009,10 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
         if (gx >= 0 && gx < w && gy >= 0 && gy < h) {
             const int64_t i = (int64_t)gy * w + gx;
             double a0, a1, a2, v0, v1, v2;
-            mg_apply_b(L, gx, gy, b2[k], [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0,
+            double Bv[6];
+            if constexpr (RC) mg_b_from(b2[k][0], b2[k][1], b2[k][2], Bv);
+            else for (int q = 0; q < 6; ++q) Bv[q] = b2[k][q];
+            mg_apply_b(L, gx, gy, Bv, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0,
                        a1, a2, v0, v1, v2);
             const double fa = fs[0][ly + 1][lx + 1], fb = fs[1][ly + 1][lx + 1], fcv = fs[2][ly + 1][lx + 1];
             r0 = fa - a0; r1 = fb - a1; r2 = fcv - a2;
@@ -1034,11 +1085,11 @@ __global__ __launch_bounds__(NT) void k_mg_down2(MGLev L, int wc, int hc, const 
 //   out = x' + omega D^-1 (f - A x') on the tile; RZ: partial f . out -> rz_part[block]
 // (Round 5: this kernel's B, f and D^-1 loaded before the prolongation stage, as k_mg_down2 does,
 // measured 0.2-1.2 us slower per launch at every level -- not kept.)
-template <bool RZ>
+template <bool RZ, bool RC = false>
 __global__ __launch_bounds__(NT) void k_mg_up2(MGLev L, int wc, int hc, const CGScal* S,
                                                const double* __restrict__ ec, const double* __restrict__ f,
                                                const double* __restrict__ xg, double* __restrict__ out,
-                                               double* __restrict__ rz_part) {
+                                               double* __restrict__ rz_part, MGCoef cf = MGCoef{}) {
     if (S->done) return;
     constexpr int RW = GT_X + 2, RH = GT_Y + 2;
     __shared__ double xs[3][RH][RW];
@@ -1072,10 +1123,18 @@ __global__ __launch_bounds__(NT) void k_mg_up2(MGLev L, int wc, int hc, const CG
         if (gx >= w || gy >= h) continue;
         const int64_t i = (int64_t)gy * w + gx;
         double a0, a1, a2, v0, v1, v2, z0, z1, z2;
-        mg_apply_t(L, gx, gy, i, [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; }, a0, a1, a2,
-                   v0, v1, v2);
+        const auto X = [&](int fl, int dy, int dx) { return xs[fl][ly + 1 + dy][lx + 1 + dx]; };
+        if constexpr (RC) {
+            double Bv[6], D[6];
+            mg_b_from(cf.fx[i], cf.fy[i], cf.f2[i], Bv);
+            mg_apply_b(L, gx, gy, Bv, X, a0, a1, a2, v0, v1, v2);
+            mg_dinv_vals(L, gx, gy, Bv, D);
+            mg_dinv_v(D, f[i] - a0, f[n + i] - a1, f[2 * n + i] - a2, z0, z1, z2);
+        } else {
+            mg_apply_t(L, gx, gy, i, X, a0, a1, a2, v0, v1, v2);
+            mg_dinv(L, i, f[i] - a0, f[n + i] - a1, f[2 * n + i] - a2, z0, z1, z2);
+        }
         const double f0 = f[i], f1 = f[n + i], f2v = f[2 * n + i];
-        mg_dinv(L, i, f0 - a0, f1 - a1, f2v - a2, z0, z1, z2);
         const double o0 = v0 + MG_OMEGA * z0, o1 = v1 + MG_OMEGA * z1, o2 = v2 + MG_OMEGA * z2;
         out[i] = o0;
         out[n + i] = o1;
@@ -1886,6 +1945,7 @@ struct foto_gn_plan {
            *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr;
     double *rr_part = nullptr, *pq_part = nullptr, *rz_part[2] = {nullptr, nullptr};
     double *r2 = nullptr, *q = nullptr, *rr_part2 = nullptr;   // the folded update (fold)
+    bool recomp = true;              // level-0 legs form B, D^-1 from fx, fy, f2 (FOTO_GN_RECOMP=0: load them)
     bool exact_tail = true;          // launch the predicted count exactly (FOTO_GN_EXACT=0: whole graphs)
     bool setup_fuse = true;          // B and block inverses per level in one pass (FOTO_GN_SETUP_FUSE=0: not)
     bool fold = true;                // k_gnp_upd folded into the level-0 down leg (FOTO_GN_FOLD=0: not)
@@ -1943,6 +2003,25 @@ static int mg_coarse_threads(const foto_gn_plan::Lev& L) {
 }
 
 // z = V(r) and the partials of r.z -> rz_out
+// level 0's legs: B and D^-1 formed from the GN coefficients (P->recomp) or loaded
+static void mg_down0(foto_gn_plan* P, int wc, int hc, double* x, double* fc, const MGUpd& upd) {
+    const auto& L = P->lev[0];
+    if (P->recomp)
+        k_mg_down2<true, true><<<mg_tiles(L.w, L.h), NT, 0, P->s>>>(P->desc(0), wc, hc, P->dS, nullptr, x, fc, upd);
+    else
+        k_mg_down2<true, false><<<mg_tiles(L.w, L.h), NT, 0, P->s>>>(P->desc(0), wc, hc, P->dS, nullptr, x, fc, upd);
+}
+
+static void mg_up0(foto_gn_plan* P, int wc, int hc, const double* e, const double* r, const double* x, double* z,
+                   double* rz_out) {
+    const auto& L = P->lev[0];
+    if (P->recomp)
+        k_mg_up2<true, true><<<mg_tiles(L.w, L.h), NT, 0, P->s>>>(P->desc(0), wc, hc, P->dS, e, r, x, z, rz_out,
+                                                                 MGCoef{P->fx, P->fy, P->d2});
+    else
+        k_mg_up2<true, false><<<mg_tiles(L.w, L.h), NT, 0, P->s>>>(P->desc(0), wc, hc, P->dS, e, r, x, z, rz_out);
+}
+
 static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out, const MGUpd* upd = nullptr) {
     hipStream_t s = P->s;
     const size_t nl = P->lev.size();
@@ -1964,7 +2043,7 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
             const auto& L = P->lev[l];
             const auto& C = P->lev[l + 1];
             if (l == 0 && upd)
-                k_mg_down2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, nullptr, L.x, C.f, *upd);
+                mg_down0(P, C.w, C.h, L.x, C.f, *upd);
             else
                 k_mg_down2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x,
                                                                    C.f, MGUpd{});
@@ -1980,7 +2059,7 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
             const auto& Lu = P->lev[l];
             const auto& Cu = P->lev[l + 1];
             if (l == 0) {
-                k_mg_up2<true><<<mg_tiles(Lu.w, Lu.h), NT, 0, s>>>(P->desc(0), Cu.w, Cu.h, P->dS, e, r, Lu.x, z, rz_out);
+                mg_up0(P, Cu.w, Cu.h, e, r, Lu.x, z, rz_out);
             } else {
                 k_mg_up2<false><<<mg_tiles(Lu.w, Lu.h), NT, 0, s>>>(P->desc(l), Cu.w, Cu.h, P->dS, e, Lu.f, Lu.x, Lu.y,
                                                                     nullptr);
@@ -1995,7 +2074,7 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
         const auto& L = P->lev[l];
         const auto& C = P->lev[l + 1];
         if (l == 0 && upd)
-            k_mg_down2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, nullptr, L.x, C.f, *upd);
+            mg_down0(P, C.w, C.h, L.x, C.f, *upd);
         else
             k_mg_down2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, l == 0 ? r : L.f, L.x,
                                                                C.f, MGUpd{});
@@ -2042,7 +2121,7 @@ static int gn_vcycle(foto_gn_plan* P, const double* r, double* z, double* rz_out
         const auto& L = P->lev[l];
         const auto& C = P->lev[l + 1];
         if (l == 0) {
-            k_mg_up2<true><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(0), C.w, C.h, P->dS, e, r, L.x, z, rz_out);
+            mg_up0(P, C.w, C.h, e, r, L.x, z, rz_out);
         } else {
             k_mg_up2<false><<<mg_tiles(L.w, L.h), NT, 0, s>>>(P->desc(l), C.w, C.h, P->dS, e, L.f, L.x, L.y, nullptr);
             e = L.y;
@@ -2067,7 +2146,8 @@ static int gn_iteration(foto_gn_plan* P, int par) {
     if (P->fold) {
         double* rold = par ? P->r2 : P->r;
         double* rnew = par ? P->r : P->r2;
-        const MGUpd U{rold, rnew, P->q, pn, P->x, rzc, P->pq_part, P->rr_part2, P->dS, P->nb_rz, P->nb_pix};
+        const MGUpd U{rold, rnew, P->q, pn, P->x, rzc, P->pq_part, P->rr_part2, P->dS, P->nb_rz, P->nb_pix,
+                      MGCoef{P->fx, P->fy, P->d2}};
         return gn_vcycle(P, rnew, P->z, P->rz_part[par ^ 1], &U);
     }
     k_gnp_upd<<<P->nb_pix, NT, 0, P->s>>>(w, h, P->fx, P->fy, P->d2, P->alpha, P->lam, pn, P->x, P->r, P->dS, rzc,
@@ -2125,6 +2205,8 @@ static int gn_plan_init(foto_gn_plan* P) {
     {
         const char* sf = getenv("FOTO_GN_SETUP_FUSE");
         P->setup_fuse = !(sf && atoi(sf) == 0);
+        const char* rc = getenv("FOTO_GN_RECOMP");
+        P->recomp = !(rc && atoi(rc) == 0);
         const char* ex = getenv("FOTO_GN_EXACT");
         P->exact_tail = !(ex && atoi(ex) == 0);
         const char* e = getenv("FOTO_GN_FOLD");

@@ -668,7 +668,8 @@ def test_gn_round5_forms_bit_identical(w, h, monkeypatch):
     arithmetic is the same in the same order, so the iterates are bit-identical (only the stop
     test's r.r is summed per tile), and the PCG counts match.  The separate form also builds the
     multigrid coefficients the round-5 way (B per level, then the block inverses per level:
-    FOTO_GN_SETUP_FUSE=0) against round 6's one pass per level."""
+    FOTO_GN_SETUP_FUSE=0) against round 6's one pass per level, and its level-0 legs load the
+    stored B and D^-1 (FOTO_GN_RECOMP=0) where round 6 forms them from fx, fy, f2 per cell."""
     from foto.synthetic import sinusoid_pair
     f1, f2 = sinusoid_pair(w, h)
     monkeypatch.setenv("FOTO_GN_PLAN_CACHE", "0")
@@ -676,6 +677,7 @@ def test_gn_round5_forms_bit_identical(w, h, monkeypatch):
     forms = (("sep", "0", "0", "0"), ("fold", "1", "0", "0"), ("ltail", "1", "0", "1"), ("ptail", "1", "1", "0"))
     for key, fold, pt, lt in forms:
         monkeypatch.setenv("FOTO_GN_SETUP_FUSE", "0" if key == "sep" else "1")
+        monkeypatch.setenv("FOTO_GN_RECOMP", "0" if key == "sep" else "1")
         monkeypatch.setenv("FOTO_GN_FOLD", fold)
         monkeypatch.setenv("FOTO_MG_PTAIL", pt)
         monkeypatch.setenv("FOTO_MG_LTAIL", lt)
