@@ -710,3 +710,48 @@ def test_gn_plan_reuse():
     with gn.Plan(w, h, alpha, lam, maxiter=5) as P:
         u, v, m, info, its = P.solve(*pairs[0])
         assert info == 5 and its == 5
+
+
+@pytest.mark.parametrize("w,h", [(2, 2), (3, 2), (97, 71)])
+def test_gn_round6_host_forms(w, h, monkeypatch):
+    """Round 6's host side of a GN solve -- the copies over a worker pool
+    (FOTO_GN_HOST_THREADS), the download in three pieces, u / v / m as views of one array, a
+    reused plan launching exactly its predicted count (FOTO_GN_EXACT) -- changes no bit against
+    the caller-alone copies and whole-graph launches, on one-level, two-level and odd
+    multi-level grids.  A reused plan whose prediction falls short after an odd number of
+    launched iterations (the parity realignment before the next graph) gives the one-shot
+    answer as well."""
+    from foto.synthetic import sinusoid_pair, textured_pair
+    alpha, lam = 0.1, 0.2
+    monkeypatch.setenv("FOTO_GN_PLAN_CACHE", "0")
+    cands = [sinusoid_pair(w, h), textured_pair(w, h), sinusoid_pair(w, h, dx=0.3, dy=0.1),
+             textured_pair(w, h, seed=3, dx=0.7, dy=0.2)]
+    ref = {}
+    for key, thr, ex in (("alone", "0", "0"), ("pool", "4", "1"), ("pool_graphs", "4", "0")):
+        monkeypatch.setenv("FOTO_GN_HOST_THREADS", thr)
+        monkeypatch.setenv("FOTO_GN_EXACT", ex)
+        ref[key] = [gn.solve(f1, f2, w, h, alpha, lam) for f1, f2 in cands]
+    for key in ("pool", "pool_graphs"):
+        for got, want in zip(ref[key], ref["alone"]):
+            assert got[3] == 0 and got[4] == want[4]
+            for a, b in zip(got[:3], want[:3]):
+                np.testing.assert_array_equal(a, b)
+    u, v, m = ref["pool"][0][:3]
+    assert u.flags.c_contiguous and v.flags.c_contiguous and m.flags.c_contiguous
+    assert not np.shares_memory(u, v) and not np.shares_memory(v, m) and u.size == v.size == m.size == w * h
+    # a plan that last needed an even count a, then a pair needing more than a + 1: it launches
+    # a + 1 (odd) iterations, then one single iteration before whole graphs
+    counts = [r[4] for r in ref["alone"]]
+    pick = [(i, j) for i in range(len(cands)) for j in range(len(cands))
+            if counts[i] % 2 == 0 and counts[j] > counts[i] + 1]
+    print(f"{w}x{h}: PCG counts {counts}, under-predicted odd pairs {pick}")
+    monkeypatch.setenv("FOTO_GN_HOST_THREADS", "4")
+    monkeypatch.setenv("FOTO_GN_EXACT", "1")
+    for i, j in pick[:2]:
+        with gn.Plan(w, h, alpha, lam) as P:
+            P.solve(*cands[i])
+            uu, vv, mm, info, its = P.solve(*cands[j])
+            t = P.timing()
+        assert info == 0 and its == counts[j] and t["launched"] >= its
+        for a, b in zip((uu, vv, mm), ref["alone"][j][:3]):
+            np.testing.assert_array_equal(a, b)
