@@ -659,7 +659,7 @@ def test_gn_solve_multilevel(pair, monkeypatch):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * max(1.0, np.abs(b).max()))
 
 
-@pytest.mark.parametrize("w,h", [(640, 480), (584, 388), (320, 240), (160, 120)])
+@pytest.mark.parametrize("w,h", [(640, 480), (584, 388), (320, 240), (160, 120), (2, 3000), (3001, 3)])
 def test_gn_round5_forms_bit_identical(w, h, monkeypatch):
     """Round 5's GN launch structures -- the PCG update folded into the level-0 down leg and the
     last level above the coarsest solved with it in one LDS-resident block (k_mg_ltail; both
