@@ -126,6 +126,47 @@ def test_c5_runsh_params_middlebury2_size_vs_oracle():
         assert np.abs(a - b).max() <= 1e-7
 
 
+EDGE_CASES = [   # (Nt, Nx, Ny, pair, r, tol, eps, max_it)
+    (2, 2, 2, "gauss", 1.0, 0.01, 1e-2, 10),
+    (2, 13, 3, "gauss", 1.0, 0.01, 1e-2, 6),
+    (3, 7, 5, "tex", 1.0, 0.01, 1e-3, 8),
+    (6, 3, 11, "tex", 2.0, 0.05, 1e-2, 6),
+]
+
+
+@pytest.mark.parametrize("mode", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("case", range(len(EDGE_CASES)))
+def test_edge_grids_vs_oracle(case, mode):
+    """The drop-in solve on edge grids -- the minimum 2x2x2 and prime / odd shapes with one axis
+    of 2 or 3 -- in every CG mode (-1: the default auto mode) against the oracle's restatement
+    of benamou_brenier.solve with the stop rules on (the reference itself is not run here:
+    DESIGN.md section 4): the same outer iteration count, CG counts +-1, crit within SURVEY.md
+    8(c)'s 1e-6 relative (measured <= 1.6e-8 on the whole sequence except one line of the 2x2x2
+    grid in the stencil modes, 2.4e-7: eight voxels, the line's criterion at 0.07), phi 1e-7 of
+    max|phi|, flow 1e-7 px."""
+    from oracle import foto_oracle as O
+    from foto.bb import solve as bb_solve
+    Nt, Nx, Ny, pair, r, tol, eps, max_it = EDGE_CASES[case]
+    if pair == "gauss":
+        rho0, rhoT = translating_gaussian(Nx, Ny)
+    else:
+        rho0, rhoT = textured_pair(Nx, Ny, seed=3, dx=1.5, dy=0.5)
+    st = {}
+    u, v, m = bb_solve(rho0, rhoT, Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=max_it, stats=st,
+                       cg_mode=mode)
+    so = {}
+    uo, vo, mo = O.solve(rho0, rhoT, Nt, Nx, Ny, r=r, convergence_tol=tol, reg_epsilon=eps, max_it=max_it, stats=so,
+                         log=lambda line: None)
+    print(f"edge {Nt}x{Nx}x{Ny} mode {mode}: {len(st['crit'])} outer (oracle {len(so['crit'])}), cg "
+          f"{list(st['cg_its'])} (oracle {so['cg_its'].tolist()}), crit rel {_rel(np.array(st['crit']), so['crit']):.1e}")
+    assert len(st["crit"]) == len(so["crit"])
+    assert np.max(np.abs(np.array(st["cg_its"]) - so["cg_its"])) <= 1
+    np.testing.assert_allclose(st["crit"], so["crit"], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(st["phi"], so["phi"], rtol=0, atol=1e-7 * max(np.abs(so["phi"]).max(), 1e-300))
+    for a, b in ((u, uo), (v, vo), (m, mo)):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
+
+
 @pytest.mark.parametrize("mode", [3, 2, 0])
 def test_c2_shape_vs_reference(gold, mode):
     d = gold("bb_c2s.npz")
