@@ -641,6 +641,23 @@ def test_gn_solve(gold):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
 
 
+@pytest.mark.parametrize("w,h", [(2, 2), (2, 9), (11, 2), (3, 5), (33, 17), (1100, 3), (5, 640)])
+def test_gn_edge_grids_vs_oracle(w, h):
+    """GN on edge grids -- the minimum 2x2, one axis of 2 or 3, odd and prime sizes, strips whose
+    hierarchy coarsens one axis down to a single cell (1100x3, 5x640) -- against the oracle's
+    spsolve (SuperLU, classical.py:126) at the goldens' 1e-7 px."""
+    from foto.synthetic import textured_pair
+    alpha, lam = 0.1, 0.2
+    f1, f2 = textured_pair(w, h, seed=5, dx=0.8, dy=0.3, smooth=1)
+    ref = O.gn_solve(f1, f2, w, h, alpha, lam)
+    u, v, m, info, its = gn.solve(f1, f2, w, h, alpha, lam)
+    err = max(np.abs(a - b).max() for a, b in zip((u, v, m), ref))
+    print(f"GN {w}x{h}: {its} PCG its, max |diff| vs spsolve {err:.1e}")
+    assert info == 0
+    for a, b in zip((u, v, m), ref):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-7)
+
+
 @pytest.mark.parametrize("pair", ["sinusoid", "textured"])
 def test_gn_solve_multilevel(pair, monkeypatch):
     """GN at 160x120 -- a four-level V-cycle (160x120 .. 20x15), which the goldens (40x30,
