@@ -403,12 +403,12 @@ def survey_bytes(k):
 
 # DESIGN.md §5's model of the time-sharded solve (each rank's compute measured as virtual shards on
 # one MI355X, plus the two all-to-alls, the halos and the all-gathers at 64 GB/s per xGMI link
-# direction and 10 us per RCCL call; profiles/r05_proxy_scaling_wt.txt, r05_proxy_scaling_c4_wt.txt):
+# direction and 10 us per RCCL call; profiles/r06_proxy_scaling.txt, r06_proxy_scaling_c4.txt):
 # the curve a measured N-GPU line is read against.  The metric grid's transposition moves more
 # bytes per link than the single GPU needs for a whole outer iteration at W = 2, so the model puts
 # W = 2 below one GPU there.
-MODEL_IT_S = {(640, 480, 32): {1: 1721, 2: 886, 4: 1729, 8: 2317},
-              (1024, 1024, 64): {1: 304, 2: 170, 4: 487, 8: 1067}}
+MODEL_IT_S = {(640, 480, 32): {1: 1815, 2: 894, 4: 1760, 8: 2388},
+              (1024, 1024, 64): {1: 309, 2: 171, 4: 491, 8: 1075}}
 C4_GRID = (1024, 1024, 64)   # BASELINE config 4: the 1024x1024 pair, 64 time steps, time-sharded
 
 

@@ -10,6 +10,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402  (the model table the line carries)
 
 pytestmark = pytest.mark.gpu
 
@@ -82,7 +84,7 @@ def _check_strong(d, n):
     assert st["items"]["a2a_staging"] == round(32 * (n - 1) / n, 4)
     assert st["alg_bytes_per_rank"] == st["alg_bytes_per_voxel"] * st["voxels_per_rank"]
     assert d["roofline"]["kernel"] == "prox" and d["roofline"]["frac"] > 0
-    assert sh["model_it_s"] == {2: 886, 4: 1729, 8: 2317}.get(n)
+    assert sh["model_it_s"] == bench.MODEL_IT_S[(640, 480, 32)].get(n)
     b = d["batch"]   # the data-parallel number: a labelled side object, never the headline
     assert b["scaling"] == "weak" and b["n_gpus"] == n and abs(b["value"] * b["ms_per_step"] / 1e3 - n) < 0.02 * n
 
